@@ -1,0 +1,132 @@
+/*
+ * splendor_beam.h — C-ABI of the MI355X Splendor beam-search step engine (libsplendor_beam.so).
+ *
+ * Drop-in boundary for ONE hot path of IamJasonBian/Splendor-RL-Gym: the per-turn state
+ * expansion of State.solve (src/solver.py:390-464) — legal-move enumeration (src/buys.py:13-41,
+ * src/gems.py:14-113), gem arithmetic (src/gems.py:116-143, src/solver.py:338-355), trail dedup
+ * (src/solver.py:425-450), heuristic scoring (src/solver.py:210-305) and the stable top-k prune
+ * to beam_width (src/solver.py:452-456).  The reference has no FFI; its boundary is the Python
+ * call surface State.solve / HEURISTICS, which the ctypes host layer
+ * (splendor-rl-gym_amd/splendor_amd/) keeps.  Each entry point below names the reference
+ * interface it replaces.
+ *
+ * Conventions: plain C types only; every call returns SB_OK (0) or a negative SB_ERR_* code,
+ * with a message from sb_last_error() (thread-local).  No exceptions or callbacks cross the ABI.
+ * The library owns all device memory and HIP streams; the caller owns every host buffer.
+ * One handle is driven by one host thread; calls block until their results are on the host.
+ *
+ * Packed speedrun state (two u64 words, also used by oracle/ and the host codec):
+ *   lo = owned-card bitmask, cards 0..63
+ *   hi = bits 0..25 cards 64..89 | bits 26+3i gems of colour i (0..7) | bits 41..48 pts
+ *        | bits 49..63 saved
+ * State identity = CPython hash((cards, gems)) as an unsigned 64-bit key (src/solver.py:318).
+ */
+#ifndef SPLENDOR_BEAM_H
+#define SPLENDOR_BEAM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SB_OK 0
+#define SB_ERR_ARG -1        /* bad argument / handle */
+#define SB_ERR_HIP -2        /* HIP runtime error (message names the call) */
+#define SB_ERR_STATE -3      /* call not valid in the handle's state (e.g. path before done) */
+#define SB_ERR_CAPACITY -4   /* visited set / buffer capacity exceeded */
+#define SB_ERR_NOTABLES -5   /* sb_init_tables not called */
+
+#define SB_HEUR_SIMPLE 0     /* simple_heuristic      src/solver.py:210-215 */
+#define SB_HEUR_BALANCED 1   /* balanced_heuristic    src/solver.py:218-249 (also 'competitive', :289-296) */
+#define SB_HEUR_AGGRESSIVE 2 /* aggressive_heuristic  src/solver.py:252-262 */
+#define SB_HEUR_EFFICIENCY 3 /* efficiency_heuristic  src/solver.py:265-286 */
+
+#define SB_N_POW_EXP 11      /* exponents {0.3,0.4,0.5,0.6,0.7,0.8,1.2,2.0,2.5,2.8,3.2} */
+#define SB_POW_BASES 256     /* integer bases 0..255 */
+
+typedef struct sb_engine sb_engine;
+
+typedef struct {
+    int32_t goal_pts;          /* State.solve(goal_pts)                src/solver.py:392 */
+    int32_t use_heuristic;     /* False = pure BFS (no noise, no prune) src/solver.py:394,452-456 */
+    int32_t heuristic;         /* SB_HEUR_*; unknown names map to simple on the host (:429) */
+    int32_t device;            /* HIP device ordinal */
+    int64_t beam_width;        /* State.solve(beam_width)              src/solver.py:396 */
+    int32_t visited_log2;      /* log2 visited-set capacity (entries); 0 = auto from beam_width */
+    int32_t flags;             /* bit 0: collect per-kernel timings into sb_step_stats */
+    /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
+    int32_t world_size;        /* 1 for single-GPU */
+    int32_t rank;
+} sb_config;
+
+typedef struct {
+    int64_t n_parents;         /* len(queue) at the start of the step */
+    int64_t n_raw;             /* successors generated (State.__iter__ yields) */
+    int64_t n_unique;          /* len(next_queue): first occurrences not in trail */
+    int64_t n_kept;            /* len(queue) after the prune */
+    int32_t done;              /* 1: a goal state was found (or the queue emptied) */
+    int32_t turn;              /* turn index the stats belong to */
+    int64_t winner_rank;       /* rank of `puzzle` in this turn's queue when done */
+    int32_t n_records;         /* max_pts records printed in this turn (src/solver.py:439-442) */
+    int32_t record_pts[32];
+    int64_t record_rank[32];
+    uint64_t noise_draws;      /* randint(1,100) draws consumed so far (= scored states) */
+    /* timings (flags bit 0): milliseconds, device-side events around each phase */
+    float ms_expand, ms_survive, ms_emit, ms_select, ms_sort, ms_gather, ms_mt, ms_total;
+} sb_step_stats;
+
+/* Host-captured exact tables (replace get_deck/get_takes/get_buys and Python's float pow):
+ *   deck_rows   90 x 7 int32: cost[5], pt, colour            (src/cardparser.py:17-66, cards.csv)
+ *   pow_tables  SB_N_POW_EXP x SB_POW_BASES doubles = float(x) ** e, captured by Python
+ *   noise       100 doubles = k * 0.01 for k = 1..100          (src/solver.py:215,247,260,284)
+ * The take-pattern table (src/gems.py:14-37) is generated inside the library. */
+int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const double* noise);
+
+/* Replaces State.solve's setup (src/solver.py:425-433): root state + random.getstate().
+ * mt_state625 = the 624 MT words + position, exactly as random.getstate()[1]. */
+int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_lo, uint64_t root_hi,
+              sb_engine** out);
+
+/* One iteration of the `while queue:` loop (src/solver.py:434-457). */
+int sb_step(sb_engine* e, sb_step_stats* out);
+
+/* Number of turns stored (turn 0 = root) and the size of one turn's queue. */
+int sb_num_turns(sb_engine* e, int32_t* out);
+int sb_turn_size(sb_engine* e, int32_t turn, int64_t* out);
+
+/* Copy queue[start:start+n] of a turn to host arrays (any pointer may be NULL).
+ * par = rank of the parent in the previous turn (the `trail` link, src/solver.py:449). */
+int sb_read_turn(sb_engine* e, int32_t turn, int64_t start, int64_t n, uint64_t* lo, uint64_t* hi,
+                 uint32_t* par, uint64_t* key);
+
+/* Root..winner path (src/solver.py:459-464).  *len = number of states written (<= cap). */
+int sb_path(sb_engine* e, uint64_t* lo, uint64_t* hi, int32_t cap, int32_t* len);
+
+/* MT19937 state after the draws consumed so far, as random.getstate()[1], so the caller's global
+ * `random` ends where the reference's would after solve(). */
+int sb_get_mt_state(sb_engine* e, uint32_t* out625);
+
+/* Visited-set entries (len(trail)). */
+int sb_visited_size(sb_engine* e, uint64_t* out);
+
+void sb_destroy(sb_engine* e);
+const char* sb_last_error(void);
+int sb_version(void);
+
+/* ---- kernel-level entry points for parity tests (same device code as sb_step) ---- */
+/* Ordered successors of n parents, stride 192 per parent: out_count[i] children for parent i. */
+int sb_debug_successors(int32_t device, const uint64_t* lo, const uint64_t* hi, int64_t n,
+                        uint64_t* out_lo, uint64_t* out_hi, uint64_t* out_key, int32_t* out_count);
+/* n tempered MT19937 words continuing from mt_state625 (device generator). */
+int sb_debug_mt_words(int32_t device, const uint32_t* mt_state625, int64_t n, uint32_t* out);
+/* Scores of n states with the given randint values k (1..100). */
+int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const uint64_t* hi,
+                    const int32_t* k, int64_t n, double* out);
+/* Stable descending sort of n u64 keys: out_idx = permutation (ties keep input order), first `keep`. */
+int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPLENDOR_BEAM_H */

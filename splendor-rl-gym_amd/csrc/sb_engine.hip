@@ -1,0 +1,1074 @@
+// sb_engine.hip — MI355X beam-search step engine for the Splendor speedrun solver.
+//
+// One sb_step() = one iteration of `while queue:` in State.solve (src/solver.py:434-457):
+//
+//   goal check      first queue state with pts >= goal wins (src/solver.py:443-445) — from the
+//                   per-pts first-rank table built by the previous step's gather (no extra pass)
+//   k_expand        block-cooperative successor enumeration (buys in deck order, then takes,
+//                   src/solver.py:357-388) into an LDS child queue; the queue is then processed
+//                   densely (one child per lane): CPython tuple hash, visited-set probe/insert and
+//                   an atomicMin claim of the child's (turn, parent rank, ordinal) tag
+//   k_survive       a child survives iff its key was new this turn AND its tag won the claim:
+//                   exactly `if next_step in trail: continue` with first-occurrence order
+//                   (src/solver.py:446-450)
+//   scan            survivor counts -> next_queue offsets (parent rank, ordinal order)
+//   k_emit          survivors' packed states, parent links and heuristic scores; the noise of
+//                   next_queue element k is the k-th accepted MT19937 draw (sb_mt.hip)
+//   top-k           stable descending sort + truncate (src/solver.py:452-456; sb_sort.hip)
+//   k_gather        the kept beam for the next turn + the per-pts first-rank table
+//
+// Visited set: open addressing over 16-byte entries {key, tag}; key = EMPTY marks a free slot.
+// The tag is (turn+1) << 40 | parent rank << 8 | ordinal; tag prefix 0 is the root's turn.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/splendor_beam.h"
+#include "sb_block.h"
+#include "sb_device.h"
+#include "sb_internal.h"
+
+namespace sb {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+static Tables g_host_tables;
+static bool g_tables_ready = false;
+
+struct Entry {
+    uint64_t key;
+    uint64_t tag;
+};
+
+constexpr int MAX_PROBE = 4096;
+
+// ------------------------------------------------------------------ visited-set probe
+// Returns true if the child is a candidate first occurrence (its tag may win the claim).
+__device__ __forceinline__ bool visit_claim(Entry* __restrict__ tab, uint64_t mask, uint64_t key, uint64_t tag,
+                                            uint32_t* slot_out, uint32_t* err) {
+    uint64_t h = mix64(key) & mask;
+    for (int probe = 0;; probe++) {
+        uint64_t k = tab[h].key;   // a stale EMPTY is resolved by the CAS; keys never change once set
+        if (k == EMPTY) {
+            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
+                                      (unsigned long long)key);
+            if (prev == EMPTY || prev == key) break;
+            k = prev;
+        }
+        if (k == key) break;
+        h = (h + 1) & mask;
+        if (probe >= MAX_PROBE) {
+            atomicOr(err, 1u);
+            *slot_out = 0xFFFFFFFFu;
+            return false;
+        }
+    }
+    *slot_out = (uint32_t)h;
+    uint64_t cur = tab[h].tag;   // stale reads only over-estimate (EMPTY or a larger same-turn tag)
+    if (cur != EMPTY && cur < tag) return false;   // seen in an earlier turn, or claimed earlier this turn
+    atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+    return true;
+}
+
+__device__ __forceinline__ uint64_t lookup_tag(const Entry* __restrict__ tab, uint64_t mask, uint64_t key) {
+    uint64_t h = mix64(key) & mask;
+    for (int probe = 0; probe <= MAX_PROBE; probe++) {
+        uint64_t k = tab[h].key;
+        if (k == key) return tab[h].tag;
+        if (k == EMPTY) return EMPTY;
+        h = (h + 1) & mask;
+    }
+    return EMPTY;
+}
+
+__global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
+    uint64_t h = mix64(key) & mask;
+    while (tab[h].key != EMPTY) h = (h + 1) & mask;
+    tab[h].key = key;
+    tab[h].tag = 0;   // turn prefix 0: in trail before the first step
+}
+
+// ------------------------------------------------------------------ k_expand
+constexpr int XP_NT = 256;            // 4 waves
+constexpr int XP_PAR = 16;            // parents per block iteration (4 per wave)
+
+struct XpShared {
+    uint32_t card[NCARDS];
+    uint32_t pat[4][NPAT_MAX];
+    int32_t npat[4];
+    uint64_t mlo[NCOL];
+    uint32_t mhi[NCOL];
+    uint64_t plo[XP_PAR], phi[XP_PAR], phc[XP_PAR];
+    int64_t prank[XP_PAR];
+    int32_t pbk[XP_PAR];
+    unsigned long long cmask[XP_PAR][3];
+    uint32_t qbuy[XP_PAR * NCARDS];
+    uint32_t qtake[XP_PAR * NPAT_MAX];
+    uint32_t nbuy, ntake, nraw;
+};
+
+__device__ __forceinline__ void load_tables_lds(const Tables* __restrict__ T, uint32_t* card, uint32_t (*pat)[NPAT_MAX],
+                                                int32_t* npat, uint64_t* mlo, uint32_t* mhi) {
+    for (int i = threadIdx.x; i < NCARDS; i += blockDim.x) card[i] = T->card[i];
+    for (int i = threadIdx.x; i < 4 * NPAT_MAX; i += blockDim.x) (&pat[0][0])[i] = (&T->pat[0][0])[i];
+    if (threadIdx.x < 4) npat[threadIdx.x] = T->npat[threadIdx.x];
+    if (threadIdx.x < NCOL) {
+        mlo[threadIdx.x] = T->colmask_lo[threadIdx.x];
+        mhi[threadIdx.x] = T->colmask_hi[threadIdx.x];
+    }
+}
+
+__device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* mhi, uint64_t lo, uint64_t hi, Derived& d) {
+    uint32_t chi = st_chi(hi);
+#pragma unroll
+    for (int i = 0; i < NCOL; i++) {
+        d.g[i] = st_gem(hi, i);
+        d.b[i] = __popcll(lo & mlo[i]) + __popc(chi & mhi[i]);
+    }
+    d.pts = st_pts(hi);
+    d.saved = st_saved(hi);
+}
+
+// Parents [0, n); for each raw child: desc byte and visited-set slot at [rank*MAX_CHILDREN + ordinal],
+// candidate bitmask (3 x u64) per parent.
+__global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
+                                                  const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
+                                                  uint64_t mask, uint64_t turn_tag, uint8_t* __restrict__ desc,
+                                                  uint32_t* __restrict__ rslot, unsigned long long* __restrict__ cand,
+                                                  unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err) {
+    __shared__ XpShared S;
+    load_tables_lds(T, S.card, S.pat, S.npat, S.mlo, S.mhi);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint64_t lt = lanemask_lt();
+    if (t == 0) S.nraw = 0;
+    for (int64_t base = (int64_t)blockIdx.x * XP_PAR; base < n; base += (int64_t)gridDim.x * XP_PAR) {
+        if (t == 0) {
+            S.nbuy = 0;
+            S.ntake = 0;
+        }
+        if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
+        __syncthreads();
+        // ---- phase A: each wave enumerates 4 parents (ballot compaction, canonical order)
+        for (int s = w; s < XP_PAR; s += XP_NT / 64) {
+            const int64_t r = base + s;
+            if (r >= n) break;
+            const uint64_t lo = blo[r], hi = bhi[r];
+            Derived d;
+            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            int ord = 0;
+            uint8_t* dr = desc + r * MAX_CHILDREN;
+#pragma unroll
+            for (int pass = 0; pass < 2; pass++) {   // buys, deck order (src/solver.py:369-374)
+                const int c = pass * 64 + lane;
+                const bool v = c < NCARDS && !st_owns(lo, hi, c) && affordable(S.card[c < NCARDS ? c : 0], d);
+                const uint64_t m = __ballot(v);
+                const int pre = __popcll(m & lt), cnt = __popcll(m);
+                uint32_t qb = 0;
+                if (lane == 0 && cnt) qb = atomicAdd(&S.nbuy, (uint32_t)cnt);
+                qb = __shfl(qb, 0, 64);
+                if (v) {
+                    const int o = ord + pre;
+                    S.qbuy[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)c << 12);
+                    dr[o] = (uint8_t)c;
+                }
+                ord += cnt;
+            }
+            const int bk = take_bucket(d);
+            if (bk >= 0) {   // takes, pattern order (src/solver.py:381-388, src/gems.py:85-108)
+                const int np = S.npat[bk];
+                for (int p0 = 0; p0 < np; p0 += 64) {
+                    const int p = p0 + lane;
+                    uint32_t gf;
+                    const bool v = p < np && take_child(S.pat[bk][p < np ? p : 0], d, &gf);
+                    const uint64_t m = __ballot(v);
+                    const int pre = __popcll(m & lt), cnt = __popcll(m);
+                    uint32_t qb = 0;
+                    if (lane == 0 && cnt) qb = atomicAdd(&S.ntake, (uint32_t)cnt);
+                    qb = __shfl(qb, 0, 64);
+                    if (v) {
+                        const int o = ord + pre;
+                        S.qtake[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)(NCARDS + p) << 12);
+                        dr[o] = (uint8_t)(NCARDS + p);
+                    }
+                    ord += cnt;
+                }
+            }
+            if (lane == 0) {
+                S.plo[s] = lo;
+                S.phi[s] = hi;
+                S.prank[s] = r;
+                S.pbk[s] = bk;
+                atomicAdd(&S.nraw, (uint32_t)ord);
+            }
+        }
+        __syncthreads();
+        // ---- parent prologue: hash(cards) of each parent, one lane each
+        if (t < XP_PAR && base + t < n) S.phc[t] = hash_cards(S.plo[t], st_chi(S.phi[t]));
+        __syncthreads();
+        // ---- phase B: dense child processing, buys first (uniform hash loops), then takes
+        const uint32_t nb = S.nbuy, tot = nb + S.ntake;
+        for (uint32_t i = t; i < tot; i += XP_NT) {
+            const uint32_t e = i < nb ? S.qbuy[i] : S.qtake[i - nb];
+            const int s = (int)(e & 15), o = (int)((e >> 4) & 255), dsc = (int)(e >> 12);
+            const uint64_t lo = S.plo[s], hi = S.phi[s];
+            uint64_t key;
+            if (dsc < NCARDS) {
+                Derived d;
+                derive_lds(S.mlo, S.mhi, lo, hi, d);
+                uint64_t clo = lo;
+                const uint64_t chi = buy_child_hi(S.card[dsc], dsc, d, hi, &clo);
+                key = state_key(hash_cards(clo, st_chi(chi)), hash_gems(st_gemfield(chi)));
+            } else {
+                Derived d;
+                derive_lds(S.mlo, S.mhi, lo, hi, d);
+                uint32_t gf;
+                take_child(S.pat[S.pbk[s]][dsc - NCARDS], d, &gf);
+                key = state_key(S.phc[s], hash_gems(gf));
+            }
+            const int64_t r = S.prank[s];
+            const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
+            uint32_t slot;
+            const bool c = visit_claim(tab, mask, key, tag, &slot, err);
+            rslot[r * MAX_CHILDREN + o] = slot;
+            if (c) atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
+        }
+        __syncthreads();
+        if (t < XP_PAR * 3) {
+            const int s = t / 3, j = t % 3;
+            if (base + s < n) cand[(base + s) * 3 + j] = S.cmask[s][j];
+        }
+        __syncthreads();
+    }
+    if (t == 0 && S.nraw) atomicAdd(nraw_total, (unsigned long long)S.nraw);
+}
+
+// ------------------------------------------------------------------ k_survive (wave per parent)
+__global__ __launch_bounds__(256) void k_survive(int64_t n, const Entry* __restrict__ tab, uint64_t turn_tag,
+                                                  const uint32_t* __restrict__ rslot,
+                                                  const unsigned long long* __restrict__ cand,
+                                                  unsigned long long* __restrict__ surv, uint32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = wg; r < n; r += nw) {
+        uint32_t total = 0;
+#pragma unroll
+        for (int pass = 0; pass < 3; pass++) {
+            const unsigned long long cm = cand[r * 3 + pass];
+            bool sv = false;
+            if ((cm >> lane) & 1ull) {
+                const int o = pass * 64 + lane;
+                const uint32_t slot = rslot[r * MAX_CHILDREN + o];
+                const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
+                sv = tab[slot].tag == tag;
+            }
+            const unsigned long long m = __ballot(sv);
+            if (lane == 0) surv[r * 3 + pass] = m;
+            total += __popcll(m);
+        }
+        if (lane == 0) cnt[r] = total;
+    }
+}
+
+// ------------------------------------------------------------------ k_emit (wave per parent)
+template <int H>
+__global__ __launch_bounds__(256) void k_emit(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
+                                              const uint64_t* __restrict__ bhi, int64_t n,
+                                              const uint8_t* __restrict__ desc,
+                                              const unsigned long long* __restrict__ surv,
+                                              const uint32_t* __restrict__ off, uint64_t* __restrict__ nlo,
+                                              uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
+                                              uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
+                                              uint64_t ring_mask, uint64_t ring_base, uint32_t* __restrict__ err) {
+    __shared__ uint32_t card[NCARDS];
+    __shared__ uint32_t pat[4][NPAT_MAX];
+    __shared__ int32_t npat[4];
+    __shared__ uint64_t mlo[NCOL];
+    __shared__ uint32_t mhi[NCOL];
+    load_tables_lds(T, card, pat, npat, mlo, mhi);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lanemask_lt();
+    const int64_t wg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = wg; r < n; r += nw) {
+        const uint64_t lo = blo[r], hi = bhi[r];
+        Derived d;
+        derive_lds(mlo, mhi, lo, hi, d);
+        const int bk = take_bucket(d);
+        uint32_t k = off[r];
+#pragma unroll
+        for (int pass = 0; pass < 3; pass++) {
+            const unsigned long long sm = surv[r * 3 + pass];
+            if (sm == 0) continue;
+            if ((sm >> lane) & 1ull) {
+                const int o = pass * 64 + lane;
+                const uint32_t kk = k + __popcll(sm & lt);
+                const int dsc = desc[r * MAX_CHILDREN + o];
+                uint64_t clo = lo, chi;
+                if (dsc < NCARDS) {
+                    chi = buy_child_hi(card[dsc], dsc, d, hi, &clo);
+                } else {
+                    uint32_t gf;
+                    take_child(pat[bk][dsc - NCARDS], d, &gf);
+                    chi = st_with_gems(hi, gf);
+                }
+                nlo[kk] = clo;
+                nhi[kk] = chi;
+                npar[kk] = (uint32_t)r;
+                if constexpr (H >= 0) {
+                    if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
+                    const int nv = ring[(ring_base + kk) & ring_mask];
+                    const double sc = score_of<H>(T->pw, *T, clo, chi, T->noise[nv - 1]);
+                    skey[kk] = (uint64_t)__double_as_longlong(sc);
+                }
+            }
+            k += __popcll(sm);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ beam write + per-pts first rank
+__global__ __launch_bounds__(256) void k_gather(const uint32_t* __restrict__ idx, int64_t m,
+                                                const uint64_t* __restrict__ nlo, const uint64_t* __restrict__ nhi,
+                                                const uint32_t* __restrict__ npar, uint64_t* __restrict__ olo,
+                                                uint64_t* __restrict__ ohi, uint32_t* __restrict__ opar,
+                                                uint32_t* __restrict__ first) {
+    __shared__ uint32_t f[256];
+    f[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = idx ? idx[i] : (uint32_t)i;
+        const uint64_t h = nhi[j];
+        olo[i] = nlo[j];
+        ohi[i] = h;
+        opar[i] = npar[j];
+        atomicMin(&f[st_pts(h)], (uint32_t)i);
+    }
+    __syncthreads();
+    if (f[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&first[threadIdx.x], f[threadIdx.x]);
+}
+
+__global__ void k_pts_first(const uint64_t* __restrict__ bhi, int64_t m, uint32_t* __restrict__ first) {
+    __shared__ uint32_t f[256];
+    f[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        atomicMin(&f[st_pts(bhi[i])], (uint32_t)i);
+    __syncthreads();
+    if (f[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&first[threadIdx.x], f[threadIdx.x]);
+}
+
+__global__ void k_keys(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi, int64_t n, uint64_t* __restrict__ key) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        key[i] = key_of(lo[i], hi[i]);
+}
+
+// ------------------------------------------------------------------ debug kernels (parity tests)
+__global__ void k_debug_succ(const Tables* __restrict__ T, const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                             int64_t n, uint64_t* olo, uint64_t* ohi, uint64_t* okey, int32_t* ocnt) {
+    __shared__ uint32_t card[NCARDS];
+    __shared__ uint32_t pat[4][NPAT_MAX];
+    __shared__ int32_t npat[4];
+    __shared__ uint64_t mlo[NCOL];
+    __shared__ uint32_t mhi[NCOL];
+    load_tables_lds(T, card, pat, npat, mlo, mhi);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lanemask_lt();
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= n) return;
+    const uint64_t plo = lo[r], phi = hi[r];
+    Derived d;
+    derive_lds(mlo, mhi, plo, phi, d);
+    const uint64_t hc = hash_cards(plo, st_chi(phi));
+    int ord = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int c = pass * 64 + lane;
+        const bool v = c < NCARDS && !st_owns(plo, phi, c) && affordable(card[c < NCARDS ? c : 0], d);
+        const uint64_t m = __ballot(v);
+        if (v) {
+            const int o = ord + __popcll(m & lt);
+            uint64_t clo = plo;
+            const uint64_t chi = buy_child_hi(card[c], c, d, phi, &clo);
+            olo[r * MAX_CHILDREN + o] = clo;
+            ohi[r * MAX_CHILDREN + o] = chi;
+            okey[r * MAX_CHILDREN + o] = state_key(hash_cards(clo, st_chi(chi)), hash_gems(st_gemfield(chi)));
+        }
+        ord += __popcll(m);
+    }
+    const int bk = take_bucket(d);
+    if (bk >= 0) {
+        const int np = npat[bk];
+        for (int p0 = 0; p0 < np; p0 += 64) {
+            const int p = p0 + lane;
+            uint32_t gf;
+            const bool v = p < np && take_child(pat[bk][p < np ? p : 0], d, &gf);
+            const uint64_t m = __ballot(v);
+            if (v) {
+                const int o = ord + __popcll(m & lt);
+                olo[r * MAX_CHILDREN + o] = plo;
+                ohi[r * MAX_CHILDREN + o] = st_with_gems(phi, gf);
+                okey[r * MAX_CHILDREN + o] = state_key(hc, hash_gems(gf));
+            }
+            ord += __popcll(m);
+        }
+    }
+    if (lane == 0) ocnt[r] = ord;
+}
+
+template <int H>
+__global__ void k_debug_scores(const Tables* __restrict__ T, const uint64_t* lo, const uint64_t* hi, const int32_t* k,
+                               int64_t n, double* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = score_of<H>(T->pw, *T, lo[i], hi[i], T->noise[k[i] - 1]);
+}
+
+// ------------------------------------------------------------------ tables
+static int npat_host(int b) { return g_host_tables.npat[b]; }
+
+static void build_patterns(Tables& T) {
+    // distinct_permutations (sorted input, lexicographic order) of the src/gems.py:22-37 patterns
+    auto add = [&](int bucket, std::vector<int> p, bool two) {
+        std::sort(p.begin(), p.end());
+        do {
+            uint32_t w = 0;
+            int two_at = 7;
+            for (int i = 0; i < NCOL; i++) {
+                w |= (uint32_t)(p[i] + 2) << (3 * i);
+                if (two && p[i] == 2 && two_at == 7) two_at = i;
+            }
+            w |= (uint32_t)two_at << 15;
+            T.pat[bucket][T.npat[bucket]++] = w;
+        } while (std::next_permutation(p.begin(), p.end()));
+    };
+    for (int b = 0; b < 4; b++) T.npat[b] = 0;
+    add(0, {1, 1, 1, 0, 0}, false);
+    add(0, {2, 0, 0, 0, 0}, true);
+    add(1, {1, 1, 1, -1, 0}, false);
+    add(1, {1, 1, 0, 0, 0}, false);
+    add(1, {2, 0, 0, 0, 0}, true);
+    add(2, {1, 1, 1, -1, -1}, false);
+    add(2, {1, 1, -1, 0, 0}, false);
+    add(2, {1, 0, 0, 0, 0}, false);
+    add(2, {2, -1, 0, 0, 0}, true);
+    add(3, {1, 1, -1, -1, 0}, false);
+    add(3, {1, -1, 0, 0, 0}, false);
+    add(3, {2, -1, -1, 0, 0}, true);
+    add(3, {2, -2, 0, 0, 0}, true);
+}
+
+// ------------------------------------------------------------------ engine
+struct Turn {
+    uint64_t* lo = nullptr;
+    uint64_t* hi = nullptr;
+    uint32_t* par = nullptr;
+    int64_t n = 0;
+};
+
+static unsigned grid_cap(int64_t work, int per_block, unsigned cap) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    return (unsigned)std::min<int64_t>(g, cap);
+}
+
+struct Engine {
+    sb_config cfg{};
+    int dev = 0;
+    hipStream_t s = nullptr, s_mt = nullptr;
+    Tables* d_tables = nullptr;
+    Entry* tab = nullptr;
+    uint64_t tab_mask = 0;
+    uint64_t visited = 1;
+    std::vector<Turn> turns;
+    DBuf<uint8_t> desc;
+    DBuf<uint32_t> rslot;
+    DBuf<unsigned long long> cand, surv;
+    DBuf<uint32_t> cnt, off;
+    DBuf<uint64_t> nlo, nhi, skey;
+    DBuf<uint32_t> npar, kidx;
+    uint32_t* d_small = nullptr;            // [0] n_unique total  [1] err  [2..] pad ; [8..8+256) first-rank table
+    unsigned long long* d_nraw = nullptr;
+    uint32_t* h_small = nullptr;            // pinned mirror of d_small (264 words)
+    unsigned long long* h_nraw = nullptr;
+    ScanScratch scan;
+    TopkScratch topk;
+    NoiseStream noise;
+    int turn = 0;
+    bool done = false;
+    int64_t winner_rank = -1;
+    int max_pts = 0;
+    hipEvent_t ev[8] = {};
+};
+
+static void check_err_word(Engine& E) {
+    uint32_t e = E.h_small[1];
+    if (e & 1u) throw HipError{hipErrorOutOfMemory, "visited set overfull (probe limit); raise visited_log2"};
+    if (e & 2u) throw HipError{hipErrorInvalidValue, "saved >= 256 exceeds the pow tables"};
+}
+
+static void read_first_table(Engine& E, const Turn& tr) {
+    // the first-rank table for the current beam was written into d_small[8..264) by gather
+    SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 264 * 4, hipMemcpyDeviceToHost, E.s));
+    SB_HIP(hipStreamSynchronize(E.s));
+    check_err_word(E);
+    (void)tr;
+}
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+static void engine_step(Engine& E, sb_step_stats* out) {
+    memset(out, 0, sizeof *out);
+    out->turn = E.turn;
+    if (E.done) {
+        out->done = 1;
+        out->winner_rank = E.winner_rank;
+        return;
+    }
+    const bool timing = E.cfg.flags & 1;
+    Turn& cur = E.turns.back();
+    const int64_t n = cur.n;
+    out->n_parents = n;
+    // ---- goal check and max_pts records, in queue order (src/solver.py:438-445)
+    read_first_table(E, cur);
+    const uint32_t* first = E.h_small + 8;
+    {
+        int64_t win = -1;
+        for (int p = E.cfg.goal_pts < 0 ? 0 : E.cfg.goal_pts; p < 256; p++)
+            if (first[p] != 0xFFFFFFFFu && (win < 0 || first[p] < (uint32_t)win)) win = first[p];
+        // records: successive minima of first[p] over p > running max, stopping at the winner
+        int64_t last_rank = -1;
+        for (;;) {
+            int64_t best = -1;
+            int bp = -1;
+            for (int p = E.max_pts + 1; p < 256; p++)
+                if (first[p] != 0xFFFFFFFFu && (best < 0 || first[p] < (uint32_t)best)) {
+                    best = first[p];
+                    bp = p;
+                }
+            if (best < 0 || (win >= 0 && best > win) || best <= last_rank) break;
+            E.max_pts = bp;
+            if (out->n_records < 32) {
+                out->record_rank[out->n_records] = best;
+                out->record_pts[out->n_records] = bp;
+                out->n_records++;
+            }
+            last_rank = best;
+        }
+        if (win >= 0) {
+            E.done = true;
+            E.winner_rank = win;
+            out->done = 1;
+            out->winner_rank = win;
+            out->noise_draws = E.noise.consumed;
+            return;
+        }
+    }
+    const bool heur = E.cfg.use_heuristic != 0;
+    // speculative noise for this step (side stream, overlaps expansion)
+    if (heur) noise_generate_async(E.noise, (uint64_t)std::max<int64_t>(n * 16, 1 << 20), E.s_mt);
+
+    if (timing) SB_HIP(hipEventRecord(E.ev[0], E.s));
+    E.desc.ensure((size_t)n * MAX_CHILDREN);
+    E.rslot.ensure((size_t)n * MAX_CHILDREN);
+    E.cand.ensure((size_t)n * 3);
+    E.surv.ensure((size_t)n * 3);
+    E.cnt.ensure((size_t)n);
+    E.off.ensure((size_t)n);
+    SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
+    const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
+    hipLaunchKernelGGL(k_expand, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo, cur.hi,
+                       n, E.tab, E.tab_mask, turn_tag, E.desc.p, E.rslot.p, E.cand.p, E.d_nraw, E.d_small + 1);
+    if (timing) SB_HIP(hipEventRecord(E.ev[1], E.s));
+    hipLaunchKernelGGL(k_survive, dim3(grid_cap(n, 4, 1u << 16)), dim3(256), 0, E.s, n, E.tab, turn_tag, E.rslot.p,
+                       E.cand.p, E.surv.p, E.cnt.p);
+    scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
+    if (timing) SB_HIP(hipEventRecord(E.ev[2], E.s));
+    SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 8, hipMemcpyDeviceToHost, E.s));
+    SB_HIP(hipMemcpyAsync(E.h_nraw, E.d_nraw, 8, hipMemcpyDeviceToHost, E.s));
+    SB_HIP(hipStreamSynchronize(E.s));
+    check_err_word(E);
+    const int64_t nu = E.h_small[0];
+    out->n_raw = (int64_t)*E.h_nraw;
+    out->n_unique = nu;
+    E.visited += (uint64_t)nu;
+    if ((double)E.visited > 0.85 * (double)(E.tab_mask + 1))
+        throw HipError{hipErrorOutOfMemory, "visited set above 85% load; raise visited_log2"};
+    if (nu == 0) {   // the queue empties: `puzzle` is the last parent expanded (src/solver.py:438,459)
+        E.done = true;
+        E.winner_rank = n - 1;
+        out->done = 1;
+        out->winner_rank = n - 1;
+        out->noise_draws = E.noise.consumed;
+        return;
+    }
+    E.nlo.ensure(nu);
+    E.nhi.ensure(nu);
+    E.npar.ensure(nu);
+    if (heur) {
+        E.skey.ensure(nu);
+        float t0 = 0;
+        (void)t0;
+        noise_ensure(E.noise, (uint64_t)nu, E.s_mt);
+    }
+    if (timing) SB_HIP(hipEventRecord(E.ev[3], E.s));
+    const unsigned eg = grid_cap(n, 4, 1u << 16);
+    const uint64_t rbase = E.noise.consumed;
+    if (!heur) {
+        hipLaunchKernelGGL(k_emit<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p,
+                           E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,
+                           E.d_small + 1);
+    } else {
+        switch (E.cfg.heuristic) {
+#define EMIT(H)                                                                                                     \
+    hipLaunchKernelGGL(k_emit<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p, \
+                       E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,    \
+                       E.d_small + 1);                                                                              \
+    break;
+            case 1: EMIT(1)
+            case 2: EMIT(2)
+            case 3: EMIT(3)
+            default: EMIT(0)
+#undef EMIT
+        }
+        E.noise.consumed += (uint64_t)nu;
+    }
+    if (timing) SB_HIP(hipEventRecord(E.ev[4], E.s));
+    // ---- prune + next beam
+    int64_t m = nu;
+    uint32_t* idx = nullptr;
+    if (heur) {
+        E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
+        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s);
+        idx = E.kidx.p;
+    }
+    if (timing) SB_HIP(hipEventRecord(E.ev[5], E.s));
+    Turn nt;
+    SB_HIP(hipMalloc((void**)&nt.lo, m * 8));
+    SB_HIP(hipMalloc((void**)&nt.hi, m * 8));
+    SB_HIP(hipMalloc((void**)&nt.par, m * 4));
+    nt.n = m;
+    SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
+    hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
+                       nt.lo, nt.hi, nt.par, E.d_small + 8);
+    if (timing) SB_HIP(hipEventRecord(E.ev[6], E.s));
+    SB_HIP(hipGetLastError());
+    E.turns.push_back(nt);
+    E.turn++;
+    out->n_kept = m;
+    out->noise_draws = E.noise.consumed;
+    if (timing) {
+        SB_HIP(hipEventSynchronize(E.ev[6]));
+        out->ms_expand = ev_ms(E.ev[0], E.ev[1]);
+        out->ms_survive = ev_ms(E.ev[1], E.ev[2]);
+        out->ms_emit = ev_ms(E.ev[3], E.ev[4]);
+        out->ms_select = ev_ms(E.ev[4], E.ev[5]);
+        out->ms_gather = ev_ms(E.ev[5], E.ev[6]);
+        out->ms_total = ev_ms(E.ev[0], E.ev[6]);
+    }
+}
+
+}  // namespace sb
+
+// ====================================================================== C-ABI
+using namespace sb;
+
+struct sb_engine {
+    Engine E;
+};
+
+template <class F>
+static int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const HipError& e) {
+        set_error(e.what);
+        return e.code == hipErrorOutOfMemory ? SB_ERR_CAPACITY : SB_ERR_HIP;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return SB_ERR_HIP;
+    }
+}
+
+extern "C" {
+
+int sb_version(void) { return 1; }
+const char* sb_last_error(void) { return g_err.c_str(); }
+
+int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const double* noise) {
+    if (!deck_rows || !pow_tables || !noise) {
+        set_error("sb_init_tables: null argument");
+        return SB_ERR_ARG;
+    }
+    Tables& T = g_host_tables;
+    memset(&T, 0, sizeof T);
+    for (int c = 0; c < NCARDS; c++) {
+        const int32_t* r = deck_rows + c * 7;
+        uint32_t w = 0;
+        for (int i = 0; i < NCOL; i++) {
+            if (r[i] < 0 || r[i] > MAXG) {
+                set_error("sb_init_tables: card cost out of range");
+                return SB_ERR_ARG;
+            }
+            w |= (uint32_t)r[i] << (3 * i);
+        }
+        if (r[5] < 0 || r[5] > 7 || r[6] < 0 || r[6] >= NCOL) {
+            set_error("sb_init_tables: card pt/colour out of range");
+            return SB_ERR_ARG;
+        }
+        w |= (uint32_t)r[5] << 15;
+        w |= (uint32_t)r[6] << 18;
+        T.card[c] = w;
+        if (c < 64) T.colmask_lo[r[6]] |= 1ull << c;
+        else T.colmask_hi[r[6]] |= 1u << (c - 64);
+    }
+    build_patterns(T);
+    memcpy(T.pw, pow_tables, sizeof T.pw);
+    memcpy(T.noise, noise, sizeof T.noise);
+    (void)npat_host;
+    g_tables_ready = true;
+    return SB_OK;
+}
+
+static Tables* upload_tables(hipStream_t st) {
+    Tables* d = nullptr;
+    SB_HIP(hipMalloc((void**)&d, sizeof(Tables)));
+    SB_HIP(hipMemcpyAsync(d, &g_host_tables, sizeof(Tables), hipMemcpyHostToDevice, st));
+    return d;
+}
+
+int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_lo, uint64_t root_hi, sb_engine** out) {
+    if (!cfg || !mt_state625 || !out) {
+        set_error("sb_create: null argument");
+        return SB_ERR_ARG;
+    }
+    if (!g_tables_ready) {
+        set_error("sb_create: call sb_init_tables first");
+        return SB_ERR_NOTABLES;
+    }
+    if (cfg->beam_width <= 0 || mt_state625[624] > 624) {
+        set_error("sb_create: bad beam_width or MT position");
+        return SB_ERR_ARG;
+    }
+    sb_engine* h = new sb_engine();
+    int rc = guarded([&]() {
+        Engine& E = h->E;
+        E.cfg = *cfg;
+        E.dev = cfg->device;
+        SB_HIP(hipSetDevice(E.dev));
+        SB_HIP(hipStreamCreateWithFlags(&E.s, hipStreamNonBlocking));
+        SB_HIP(hipStreamCreateWithFlags(&E.s_mt, hipStreamNonBlocking));
+        for (auto& e : E.ev) SB_HIP(hipEventCreate(&e));
+        E.d_tables = upload_tables(E.s);
+        int lg = cfg->visited_log2;
+        if (lg <= 0) {
+            // ~10 unique children per parent per turn, ~20 turns, <= 50% load
+            double want = (double)cfg->beam_width * 10.0 * 20.0 * 2.0;
+            lg = 20;
+            while ((double)(1ull << lg) < want && lg < 31) lg++;
+        }
+        if (lg < 10 || lg > 32) throw HipError{hipErrorInvalidValue, "visited_log2 out of range [10, 32]"};
+        const uint64_t cap = 1ull << lg;
+        E.tab_mask = cap - 1;
+        SB_HIP(hipMalloc((void**)&E.tab, cap * sizeof(Entry)));
+        SB_HIP(hipMemsetAsync(E.tab, 0xFF, cap * sizeof(Entry), E.s));
+        SB_HIP(hipMalloc((void**)&E.d_small, 264 * 4));
+        SB_HIP(hipMalloc((void**)&E.d_nraw, 8));
+        SB_HIP(hipHostMalloc((void**)&E.h_small, 264 * 4, hipHostMallocDefault));
+        SB_HIP(hipHostMalloc((void**)&E.h_nraw, 8, hipHostMallocDefault));
+        SB_HIP(hipMemsetAsync(E.d_small, 0, 264 * 4, E.s));
+        // root: turn 0, visited = {root}
+        Turn t0;
+        SB_HIP(hipMalloc((void**)&t0.lo, 8));
+        SB_HIP(hipMalloc((void**)&t0.hi, 8));
+        SB_HIP(hipMalloc((void**)&t0.par, 4));
+        uint32_t nopar = 0xFFFFFFFFu;
+        SB_HIP(hipMemcpyAsync(t0.lo, &root_lo, 8, hipMemcpyHostToDevice, E.s));
+        SB_HIP(hipMemcpyAsync(t0.hi, &root_hi, 8, hipMemcpyHostToDevice, E.s));
+        SB_HIP(hipMemcpyAsync(t0.par, &nopar, 4, hipMemcpyHostToDevice, E.s));
+        t0.n = 1;
+        E.turns.push_back(t0);
+        hipLaunchKernelGGL(k_insert_root, dim3(1), dim3(1), 0, E.s, E.tab, E.tab_mask, key_of(root_lo, root_hi));
+        SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
+        hipLaunchKernelGGL(k_pts_first, dim3(1), dim3(256), 0, E.s, t0.hi, (int64_t)1, E.d_small + 8);
+        uint64_t ring = 1ull << 24;
+        while (ring < (uint64_t)cfg->beam_width * 64 && ring < (1ull << 34)) ring <<= 1;
+        noise_init(E.noise, mt_state625, ring, E.s);
+        SB_HIP(hipStreamSynchronize(E.s));
+        return SB_OK;
+    });
+    if (rc != SB_OK) {
+        sb_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return SB_OK;
+}
+
+int sb_step(sb_engine* h, sb_step_stats* out) {
+    if (!h || !out) {
+        set_error("sb_step: null argument");
+        return SB_ERR_ARG;
+    }
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(h->E.dev));
+        engine_step(h->E, out);
+        return SB_OK;
+    });
+}
+
+int sb_num_turns(sb_engine* h, int32_t* out) {
+    if (!h || !out) return SB_ERR_ARG;
+    *out = (int32_t)h->E.turns.size();
+    return SB_OK;
+}
+
+int sb_turn_size(sb_engine* h, int32_t turn, int64_t* out) {
+    if (!h || !out || turn < 0 || turn >= (int32_t)h->E.turns.size()) {
+        set_error("sb_turn_size: bad turn");
+        return SB_ERR_ARG;
+    }
+    *out = h->E.turns[turn].n;
+    return SB_OK;
+}
+
+int sb_read_turn(sb_engine* h, int32_t turn, int64_t start, int64_t n, uint64_t* lo, uint64_t* hi, uint32_t* par,
+                 uint64_t* key) {
+    if (!h || turn < 0 || turn >= (int32_t)h->E.turns.size()) {
+        set_error("sb_read_turn: bad turn");
+        return SB_ERR_ARG;
+    }
+    Engine& E = h->E;
+    const Turn& t = E.turns[turn];
+    if (start < 0 || n < 0 || start + n > t.n) {
+        set_error("sb_read_turn: range out of bounds");
+        return SB_ERR_ARG;
+    }
+    if (n == 0) return SB_OK;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(E.dev));
+        if (lo) SB_HIP(hipMemcpyAsync(lo, t.lo + start, n * 8, hipMemcpyDeviceToHost, E.s));
+        if (hi) SB_HIP(hipMemcpyAsync(hi, t.hi + start, n * 8, hipMemcpyDeviceToHost, E.s));
+        if (par) SB_HIP(hipMemcpyAsync(par, t.par + start, n * 4, hipMemcpyDeviceToHost, E.s));
+        if (key) {
+            uint64_t* dk = nullptr;
+            SB_HIP(hipMalloc((void**)&dk, n * 8));
+            hipLaunchKernelGGL(k_keys, dim3(grid_cap(n, 256, 4096)), dim3(256), 0, E.s, t.lo + start, t.hi + start, n, dk);
+            SB_HIP(hipMemcpyAsync(key, dk, n * 8, hipMemcpyDeviceToHost, E.s));
+            SB_HIP(hipStreamSynchronize(E.s));
+            SB_HIP(hipFree(dk));
+        }
+        SB_HIP(hipStreamSynchronize(E.s));
+        return SB_OK;
+    });
+}
+
+int sb_path(sb_engine* h, uint64_t* lo, uint64_t* hi, int32_t cap, int32_t* len) {
+    if (!h || !lo || !hi || !len) return SB_ERR_ARG;
+    Engine& E = h->E;
+    if (!E.done) {
+        set_error("sb_path: search not finished");
+        return SB_ERR_STATE;
+    }
+    const int T = (int)E.turns.size();
+    if (cap < T) {
+        set_error("sb_path: cap too small");
+        return SB_ERR_ARG;
+    }
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(E.dev));
+        int64_t r = E.winner_rank;
+        for (int t = T - 1; t >= 0; t--) {
+            uint32_t p = 0;
+            SB_HIP(hipMemcpy(&lo[t], E.turns[t].lo + r, 8, hipMemcpyDeviceToHost));
+            SB_HIP(hipMemcpy(&hi[t], E.turns[t].hi + r, 8, hipMemcpyDeviceToHost));
+            SB_HIP(hipMemcpy(&p, E.turns[t].par + r, 4, hipMemcpyDeviceToHost));
+            r = p;
+        }
+        *len = T;
+        return SB_OK;
+    });
+}
+
+int sb_get_mt_state(sb_engine* h, uint32_t* out625) {
+    if (!h || !out625) return SB_ERR_ARG;
+    noise_mt_state(h->E.noise, out625);
+    return SB_OK;
+}
+
+int sb_visited_size(sb_engine* h, uint64_t* out) {
+    if (!h || !out) return SB_ERR_ARG;
+    *out = h->E.visited;
+    return SB_OK;
+}
+
+void sb_destroy(sb_engine* h) {
+    if (!h) return;
+    Engine& E = h->E;
+    (void)hipSetDevice(E.dev);
+    if (E.s) (void)hipStreamSynchronize(E.s);
+    if (E.s_mt) (void)hipStreamSynchronize(E.s_mt);
+    for (auto& t : E.turns) {
+        (void)hipFree(t.lo);
+        (void)hipFree(t.hi);
+        (void)hipFree(t.par);
+    }
+    E.desc.release();
+    E.rslot.release();
+    E.cand.release();
+    E.surv.release();
+    E.cnt.release();
+    E.off.release();
+    E.nlo.release();
+    E.nhi.release();
+    E.skey.release();
+    E.npar.release();
+    E.kidx.release();
+    E.scan.tiles.release();
+    E.topk.k0.release();
+    E.topk.k1.release();
+    E.topk.v0.release();
+    E.topk.v1.release();
+    E.topk.tile_hist.release();
+    E.topk.tile_a.release();
+    E.topk.tile_b.release();
+    E.topk.small.release();
+    E.topk.scan.tiles.release();
+    if (E.topk.h_flags) (void)hipHostFree(E.topk.h_flags);
+    noise_free(E.noise);
+    if (E.tab) (void)hipFree(E.tab);
+    if (E.d_tables) (void)hipFree(E.d_tables);
+    if (E.d_small) (void)hipFree(E.d_small);
+    if (E.d_nraw) (void)hipFree(E.d_nraw);
+    if (E.h_small) (void)hipHostFree(E.h_small);
+    if (E.h_nraw) (void)hipHostFree(E.h_nraw);
+    for (auto& e : E.ev)
+        if (e) (void)hipEventDestroy(e);
+    if (E.s) (void)hipStreamDestroy(E.s);
+    if (E.s_mt) (void)hipStreamDestroy(E.s_mt);
+    delete h;
+}
+
+int sb_debug_successors(int32_t device, const uint64_t* lo, const uint64_t* hi, int64_t n, uint64_t* out_lo,
+                        uint64_t* out_hi, uint64_t* out_key, int32_t* out_count) {
+    if (!g_tables_ready) {
+        set_error("call sb_init_tables first");
+        return SB_ERR_NOTABLES;
+    }
+    if (n <= 0) return SB_OK;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(device));
+        Tables* dt = upload_tables(0);
+        uint64_t *dlo, *dhi, *olo, *ohi, *okey;
+        int32_t* ocnt;
+        const size_t m = (size_t)n * MAX_CHILDREN;
+        SB_HIP(hipMalloc((void**)&dlo, n * 8));
+        SB_HIP(hipMalloc((void**)&dhi, n * 8));
+        SB_HIP(hipMalloc((void**)&olo, m * 8));
+        SB_HIP(hipMalloc((void**)&ohi, m * 8));
+        SB_HIP(hipMalloc((void**)&okey, m * 8));
+        SB_HIP(hipMalloc((void**)&ocnt, n * 4));
+        SB_HIP(hipMemcpy(dlo, lo, n * 8, hipMemcpyHostToDevice));
+        SB_HIP(hipMemcpy(dhi, hi, n * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_debug_succ, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, 0, dt, dlo, dhi, n, olo, ohi, okey, ocnt);
+        SB_HIP(hipGetLastError());
+        SB_HIP(hipMemcpy(out_lo, olo, m * 8, hipMemcpyDeviceToHost));
+        SB_HIP(hipMemcpy(out_hi, ohi, m * 8, hipMemcpyDeviceToHost));
+        SB_HIP(hipMemcpy(out_key, okey, m * 8, hipMemcpyDeviceToHost));
+        SB_HIP(hipMemcpy(out_count, ocnt, n * 4, hipMemcpyDeviceToHost));
+        for (void* p : {(void*)dlo, (void*)dhi, (void*)olo, (void*)ohi, (void*)okey, (void*)ocnt, (void*)dt}) SB_HIP(hipFree(p));
+        return SB_OK;
+    });
+}
+
+int sb_debug_mt_words(int32_t device, const uint32_t* mt_state625, int64_t n, uint32_t* out) {
+    if (!mt_state625 || !out || n < 0) return SB_ERR_ARG;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(device));
+        mt_debug_words(mt_state625, n, out);
+        return SB_OK;
+    });
+}
+
+int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const uint64_t* hi, const int32_t* k,
+                    int64_t n, double* out) {
+    if (!g_tables_ready) {
+        set_error("call sb_init_tables first");
+        return SB_ERR_NOTABLES;
+    }
+    if (n <= 0) return SB_OK;
+    for (int64_t i = 0; i < n; i++)
+        if (k[i] < 1 || k[i] > 100) {
+            set_error("sb_debug_scores: k out of 1..100");
+            return SB_ERR_ARG;
+        }
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(device));
+        Tables* dt = upload_tables(0);
+        uint64_t *dlo, *dhi;
+        int32_t* dk;
+        double* dout;
+        SB_HIP(hipMalloc((void**)&dlo, n * 8));
+        SB_HIP(hipMalloc((void**)&dhi, n * 8));
+        SB_HIP(hipMalloc((void**)&dk, n * 4));
+        SB_HIP(hipMalloc((void**)&dout, n * 8));
+        SB_HIP(hipMemcpy(dlo, lo, n * 8, hipMemcpyHostToDevice));
+        SB_HIP(hipMemcpy(dhi, hi, n * 8, hipMemcpyHostToDevice));
+        SB_HIP(hipMemcpy(dk, k, n * 4, hipMemcpyHostToDevice));
+        dim3 g((unsigned)((n + 255) / 256));
+        switch (heuristic) {
+            case 1: hipLaunchKernelGGL(k_debug_scores<1>, g, dim3(256), 0, 0, dt, dlo, dhi, dk, n, dout); break;
+            case 2: hipLaunchKernelGGL(k_debug_scores<2>, g, dim3(256), 0, 0, dt, dlo, dhi, dk, n, dout); break;
+            case 3: hipLaunchKernelGGL(k_debug_scores<3>, g, dim3(256), 0, 0, dt, dlo, dhi, dk, n, dout); break;
+            default: hipLaunchKernelGGL(k_debug_scores<0>, g, dim3(256), 0, 0, dt, dlo, dhi, dk, n, dout); break;
+        }
+        SB_HIP(hipGetLastError());
+        SB_HIP(hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost));
+        for (void* p : {(void*)dlo, (void*)dhi, (void*)dk, (void*)dout, (void*)dt}) SB_HIP(hipFree(p));
+        return SB_OK;
+    });
+}
+
+int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx) {
+    if (!keys || !out_idx || n < 0 || keep < 0) return SB_ERR_ARG;
+    if (n == 0 || keep == 0) return SB_OK;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(device));
+        hipStream_t st;
+        SB_HIP(hipStreamCreate(&st));
+        uint64_t* dk;
+        uint32_t* di;
+        const int64_t m = std::min(n, keep);
+        SB_HIP(hipMalloc((void**)&dk, n * 8));
+        SB_HIP(hipMalloc((void**)&di, m * 4));
+        SB_HIP(hipMemcpy(dk, keys, n * 8, hipMemcpyHostToDevice));
+        TopkScratch s;
+        topk_stable_desc(dk, n, keep, di, s, st);
+        SB_HIP(hipStreamSynchronize(st));
+        SB_HIP(hipMemcpy(out_idx, di, m * 4, hipMemcpyDeviceToHost));
+        SB_HIP(hipFree(dk));
+        SB_HIP(hipFree(di));
+        s.k0.release();
+        s.k1.release();
+        s.v0.release();
+        s.v1.release();
+        s.tile_hist.release();
+        s.tile_a.release();
+        s.tile_b.release();
+        s.small.release();
+        s.scan.tiles.release();
+        if (s.h_flags) (void)hipHostFree(s.h_flags);
+        SB_HIP(hipStreamDestroy(st));
+        return SB_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// sb_internal.h — host-side declarations shared by the engine's translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace sb {
+
+// ---- error plumbing: every HIP call in the library goes through SB_HIP ----
+void set_error(const std::string& msg);
+struct HipError {
+    hipError_t code;
+    std::string what;
+};
+#define SB_HIP(call)                                                                                        \
+    do {                                                                                                    \
+        hipError_t _e = (call);                                                                             \
+        if (_e != hipSuccess)                                                                               \
+            throw ::sb::HipError{_e, std::string(#call) + " -> " + hipGetErrorString(_e) + " @" __FILE__ ":" + \
+                                         std::to_string(__LINE__)};                                         \
+    } while (0)
+
+// ---- device buffer helper (grow-only) ----
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (p) SB_HIP(hipFree(p));
+        size_t c = n < 1024 ? 1024 : n;
+        SB_HIP(hipMalloc((void**)&p, c * sizeof(T)));
+        cap = c;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// ---- scan (sb_scan.hip) ----
+struct ScanScratch {
+    DBuf<uint32_t> tiles;
+};
+constexpr int SCAN_TILE = 4096;
+// exclusive scan of n u32 values (in may equal out); *total_dev (u32, device) receives the sum
+// single-workgroup exclusive scan of a short array in place (tile sums); *total_dev gets the sum
+void scan_tiles_inplace(uint32_t* tiles, int64_t ntiles, uint32_t* total_dev, hipStream_t st);
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev, ScanScratch& s,
+                        hipStream_t st);
+
+// ---- stable top-k (sb_sort.hip) ----
+struct TopkScratch {
+    DBuf<uint64_t> k0, k1;          // keys ping-pong
+    DBuf<uint32_t> v0, v1;          // payload ping-pong
+    DBuf<uint32_t> tile_hist;       // 256 x ntiles
+    DBuf<uint32_t> tile_a, tile_b;  // compaction counts
+    DBuf<uint64_t> small;           // select state + global histograms
+    uint32_t* h_flags = nullptr;    // pinned
+    ScanScratch scan;
+};
+// Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.
+// Returns the number written (min(n, keep)).  ms_select/ms_sort get device times if non-null.
+int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
+                         hipStream_t st);
+
+// ---- MT19937 noise stream (sb_mt.hip) ----
+struct HostMT {
+    uint32_t mt[624];
+    int idx;
+    uint32_t next();
+};
+struct NoiseStream {
+    uint32_t* d_state = nullptr;   // 624 words, device generator state (always at a block boundary)
+    DBuf<uint32_t> raw;            // raw tempered words staging
+    DBuf<uint8_t> ring;            // accepted randint values 1..100
+    uint64_t ring_mask = 0;
+    uint64_t produced = 0;         // accepted values written so far (host mirror, valid after sync)
+    uint64_t consumed = 0;         // accepted values consumed by emitted states
+    uint32_t* d_total = nullptr;   // device counter of accepted values from the last compaction
+    uint32_t* h_total = nullptr;   // pinned mirror
+    HostMT initial;                // state at sb_create (for sb_get_mt_state replay)
+    HostMT replay;                 // replay cursor
+    uint64_t replay_draws = 0;
+    ScanScratch scan;
+    hipEvent_t ev_ready = nullptr;
+    bool pending = false;
+    uint64_t pending_words = 0;
+};
+void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, hipStream_t st);
+// Launch generation of >= `words` raw words + compaction on stream st (asynchronous).
+void noise_generate_async(NoiseStream& ns, uint64_t words, hipStream_t st);
+// Block until the ring holds >= need unconsumed values (generating more if necessary).
+void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st);
+void noise_free(NoiseStream& ns);
+void noise_mt_state(NoiseStream& ns, uint32_t* out625);
+// debug: raw device words
+void mt_debug_words(const uint32_t* state625, int64_t n, uint32_t* out);
+
+}  // namespace sb

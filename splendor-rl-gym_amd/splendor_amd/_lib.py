@@ -1,0 +1,144 @@
+"""ctypes binding of ``libsplendor_beam.so`` (declared in ``include/splendor_beam.h``).
+
+The product path has exactly one implementation: the HIP engine.  If the shared
+library is missing or the GPU is unavailable, every entry point raises — there is
+no CPU fallback (the CPU restatement under ``oracle/`` is test infrastructure).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(PKG_DIR), 'csrc')
+LIB_PATH = os.path.join(PKG_DIR, 'libsplendor_beam.so')
+SOURCES = ['sb_engine.hip', 'sb_scan.hip', 'sb_sort.hip', 'sb_mt.hip']
+
+SB_OK = 0
+SB_ERR_ARG = -1
+SB_ERR_HIP = -2
+SB_ERR_STATE = -3
+SB_ERR_CAPACITY = -4
+SB_ERR_NOTABLES = -5
+
+# exponents of the host-captured pow tables, in SB row order (include/splendor_beam.h)
+POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
+POW_BASES = 256
+EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
+            'sb_get_mt_state', 'sb_visited_size', 'sb_destroy', 'sb_last_error', 'sb_version',
+            'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_scores', 'sb_debug_topk')
+
+
+class SplendorBeamError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f'[{code}] {msg}')
+        self.code = code
+
+
+class SbConfig(C.Structure):
+    _fields_ = [('goal_pts', C.c_int32), ('use_heuristic', C.c_int32), ('heuristic', C.c_int32),
+                ('device', C.c_int32), ('beam_width', C.c_int64), ('visited_log2', C.c_int32),
+                ('flags', C.c_int32), ('world_size', C.c_int32), ('rank', C.c_int32)]
+
+
+class SbStepStats(C.Structure):
+    _fields_ = [('n_parents', C.c_int64), ('n_raw', C.c_int64), ('n_unique', C.c_int64), ('n_kept', C.c_int64),
+                ('done', C.c_int32), ('turn', C.c_int32), ('winner_rank', C.c_int64), ('n_records', C.c_int32),
+                ('record_pts', C.c_int32 * 32), ('record_rank', C.c_int64 * 32), ('noise_draws', C.c_uint64),
+                ('ms_expand', C.c_float), ('ms_survive', C.c_float), ('ms_emit', C.c_float),
+                ('ms_select', C.c_float), ('ms_sort', C.c_float), ('ms_gather', C.c_float), ('ms_mt', C.c_float),
+                ('ms_total', C.c_float)]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ('record_pts', 'record_rank')}
+        d['records'] = [(self.record_rank[i], self.record_pts[i]) for i in range(self.n_records)]
+        d['done'] = bool(self.done)
+        return d
+
+
+def build(verbose: bool = False) -> str:
+    """Compile the HIP sources for gfx950 into the in-tree shared library."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = ['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',
+           '-Wall', '-Wno-unused-function', *srcs, '-o', LIB_PATH]
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] if os.path.isdir(CSRC) else []
+    deps.append(os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), 'include', 'splendor_beam.h'))
+    return any(os.path.exists(p) and os.path.getmtime(p) > t for p in deps)
+
+
+_lib = None
+_tables_ready = False
+
+
+def lib():
+    """Load (never silently replace) the engine library."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f'{LIB_PATH} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)')
+        L = C.CDLL(LIB_PATH)
+        u64p = np.ctypeslib.ndpointer(np.uint64, flags='C')
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags='C')
+        i32p = np.ctypeslib.ndpointer(np.int32, flags='C')
+        f64p = np.ctypeslib.ndpointer(np.float64, flags='C')
+        vp = C.c_void_p
+        L.sb_init_tables.argtypes = [i32p, f64p, f64p]
+        L.sb_create.argtypes = [C.POINTER(SbConfig), u32p, C.c_uint64, C.c_uint64, C.POINTER(vp)]
+        L.sb_step.argtypes = [vp, C.POINTER(SbStepStats)]
+        L.sb_num_turns.argtypes = [vp, C.POINTER(C.c_int32)]
+        L.sb_turn_size.argtypes = [vp, C.c_int32, C.POINTER(C.c_int64)]
+        L.sb_read_turn.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, vp, vp, vp, vp]
+        L.sb_path.argtypes = [vp, u64p, u64p, C.c_int32, C.POINTER(C.c_int32)]
+        L.sb_get_mt_state.argtypes = [vp, u32p]
+        L.sb_visited_size.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.sb_destroy.argtypes = [vp]
+        L.sb_destroy.restype = None
+        L.sb_last_error.restype = C.c_char_p
+        L.sb_debug_successors.argtypes = [C.c_int32, u64p, u64p, C.c_int64, u64p, u64p, u64p, i32p]
+        L.sb_debug_mt_words.argtypes = [C.c_int32, u32p, C.c_int64, u32p]
+        L.sb_debug_scores.argtypes = [C.c_int32, C.c_int32, u64p, u64p, i32p, C.c_int64, f64p]
+        L.sb_debug_topk.argtypes = [C.c_int32, u64p, C.c_int64, C.c_int64, u32p]
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ''):
+    if rc != SB_OK:
+        msg = lib().sb_last_error().decode(errors='replace')
+        raise SplendorBeamError(rc, f'{what}: {msg}' if what else msg)
+
+
+def pow_tables() -> np.ndarray:
+    """float(x) ** e for the heuristics' exponents — Python's own float pow (libm), captured exactly."""
+    t = np.empty((len(POW_EXPONENTS), POW_BASES), dtype=np.float64)
+    for r, e in enumerate(POW_EXPONENTS):
+        for x in range(POW_BASES):
+            t[r, x] = x ** e
+    return t
+
+
+def noise_table() -> np.ndarray:
+    """randint(1, 100) * 0.01 for k = 1..100 (src/solver.py:215)."""
+    return np.array([k * 0.01 for k in range(1, 101)], dtype=np.float64)
+
+
+def ensure_tables():
+    global _tables_ready
+    if not _tables_ready:
+        from .deck import deck_rows
+        check(lib().sb_init_tables(np.array(deck_rows(), dtype=np.int32), np.ascontiguousarray(pow_tables().ravel()),
+                                   noise_table()), 'sb_init_tables')
+        _tables_ready = True

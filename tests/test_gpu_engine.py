@@ -1,0 +1,181 @@
+"""GPU parity tests: the HIP engine (through the C-ABI) against the CPU oracle and the reference's goldens.
+
+Bit-exact bar: successor lists, keys, scores (float64 bits), MT words, per-turn beams
+(keys + parent links), solution paths and the final MT19937 state.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_c
+from conftest import golden, golden_exists
+from splendor_amd import codec
+from splendor_amd.engine import BeamEngine, device_mt_words, device_scores, device_successors, device_topk
+
+pytestmark = pytest.mark.gpu
+
+
+def _mt(seed):
+    random.seed(seed)
+    return random.getstate()[1]
+
+
+# ---------------------------------------------------------------- kernels
+def test_device_successors_golden(tables):
+    """k_expand enumeration == reference State.__iter__ (order, states, hash) on the captured parents."""
+    par = [s['parent'] for s in tables['successors']]
+    lo, hi = zip(*[codec.encode(p[0], p[2], p[3], p[4]) for p in par])
+    out = device_successors(lo, hi)
+    for s, (clo, chi, ckey) in zip(tables['successors'], out):
+        got = [(*codec.decode(int(a), int(b)), codec.to_signed(int(k))) for a, b, k in zip(clo, chi, ckey)]
+        exp = [(tuple(c[0]), tuple(c[1]), tuple(c[2]), c[3], c[4], c[5]) for c in s['children']]
+        assert got == exp
+
+
+def test_device_successors_random_vs_oracle():
+    """Random reachable-ish states (all gem totals 0..10, 0..25 cards)."""
+    rng = np.random.default_rng(1)
+    lo, hi = [], []
+    for _ in range(3000):
+        cards = sorted(rng.choice(90, rng.integers(0, 26), replace=False).tolist())
+        while True:
+            gems = rng.integers(0, 8, 5).tolist()
+            if sum(gems) <= 10:
+                break
+        a, b = codec.encode(cards, gems, int(rng.integers(0, 40)), int(rng.integers(0, 200)))
+        lo.append(a)
+        hi.append(b)
+    out = device_successors(lo, hi)
+    L = oracle_c.lib()
+    olo = np.zeros(256, np.uint64)
+    ohi = np.zeros(256, np.uint64)
+    okey = np.zeros(256, np.uint64)
+    for i, (clo, chi, ckey) in enumerate(out):
+        n = L.oc_successors(lo[i], hi[i], olo, ohi, okey)
+        assert n == len(clo)
+        assert np.array_equal(clo, olo[:n]) and np.array_equal(chi, ohi[:n]) and np.array_equal(ckey, okey[:n])
+
+
+def test_device_mt_words(tables):
+    for seed, v in tables['mt'].items():
+        st = np.array(v['state'], np.uint32)
+        w = device_mt_words(st, 2000)
+        assert w.tolist() == v['words']
+    # a long run crossing many device twists vs the oracle's host MT
+    random.seed(777)
+    for _ in range(313):
+        random.getrandbits(32)
+    st = random.getstate()[1]
+    w = device_mt_words(st, 200_000)
+    ref = np.zeros(200_000, np.uint32)
+    oracle_c.lib().oc_mt_words(np.array(st, np.uint32), ref, 200_000)
+    assert np.array_equal(w, ref)
+
+
+@pytest.mark.parametrize('hid,name', [(0, 'simple'), (1, 'balanced'), (2, 'aggressive'), (3, 'efficiency'),
+                                      (1, 'competitive')])
+def test_device_scores_golden(tables, hid, name):
+    rows = tables['heuristic_scores_seed11']
+    random.seed(11)
+    k = random.randint(1, 100)
+    lo, hi = zip(*[codec.encode(r['cards'], r['gems'], r['pts'], r['saved']) for r in rows])
+    got = device_scores(hid, lo, hi, [k] * len(rows))
+    assert [float(x).hex() for x in got] == [r[name] for r in rows]
+
+
+def test_device_topk_stable():
+    rng = np.random.default_rng(5)
+    for n, keep, distinct in [(1, 1, 1), (1000, 10, 3), (50_000, 7_000, 40), (300_000, 300_000, 1000),
+                              (1_000_000, 123_457, 2500), (200_000, 1, 5), (70_000, 69_999, 2)]:
+        vals = rng.choice(rng.random(distinct) * 1e4 + 0.01, n)
+        keys = vals.astype(np.float64).view(np.uint64)
+        exp = np.argsort(-vals, kind='stable')[:keep]
+        got = device_topk(keys, keep)
+        assert np.array_equal(got, exp.astype(np.uint32)), (n, keep, distinct)
+
+
+# ---------------------------------------------------------------- whole solves
+def _run_pair(goal, heur, width, seed, use_heuristic=True):
+    from splendor_amd.engine import HEURISTIC_IDS
+    st = _mt(seed)
+    eng = BeamEngine(goal_pts=goal, use_heuristic=use_heuristic, heuristic=HEURISTIC_IDS.get(heur, 0),
+                     beam_width=width, mt_state625=st)
+    return eng, st
+
+
+def _skey(lo, hi):
+    cards, _, gems, _, _ = codec.decode(lo, hi)
+    return codec.to_signed(codec.state_key(cards, gems))
+
+
+def _check_against_golden(g):
+    eng, _ = _run_pair(g['goal'], g['heuristic'], g['beam_width'], g['seed'])
+    turns = [t for t in g['turns'] if t['n_unique'] > 0]
+    t = 0
+    while True:
+        stt = eng.step()
+        if stt['done']:
+            break
+        t += 1
+        exp = turns[t - 1]
+        assert stt['n_unique'] == exp['n_unique'], t
+        _, _, _, key = eng.read_turn(t)
+        assert len(key) == exp['n_kept'] and oracle_c.beam_digest(key) == exp['digest'], f'turn {t}'
+    assert t == len(turns)
+    path = eng.path()
+    assert [_skey(a, b) for a, b in path] == [p[5] for p in g['path']]
+    assert oracle_c.mt_fingerprint(eng.mt_state()) == g['final_mt']
+    eng.close()
+
+
+def test_solves_small_golden():
+    for g in golden('solves_small.json'):
+        _check_against_golden(g)
+
+
+@pytest.mark.parametrize('name', ['solve_g10_simple_w300000_s0.json', 'solve_g15_simple_w300000_s0.json',
+                                  'solve_g15_balanced_w300000_s0.json', 'solve_g15_aggressive_w300000_s0.json',
+                                  'solve_g15_efficiency_w300000_s0.json'])
+def test_solve_w300k_golden(name):
+    if not golden_exists(name):
+        pytest.skip(f'{name} not captured')
+    _check_against_golden(golden(name))
+
+
+def test_bfs_golden():
+    for g in golden('bfs.json'):
+        eng = BeamEngine(goal_pts=g['goal'], use_heuristic=False, heuristic=0, beam_width=1, mt_state625=_mt(0))
+        while not eng.step()['done']:
+            pass
+        path = [repr_state(a, b) for a, b in eng.path()]
+        assert path == [p[4] for p in g['path']]
+        eng.close()
+
+
+def repr_state(lo, hi):
+    from splendor_amd.solver import State
+    return repr(State.from_packed(lo, hi))
+
+
+def test_vs_oracle_stepwise_random_configs():
+    """Per-turn beams (keys AND parent links) identical to the C oracle over several configs."""
+    for goal, heur, width, seed in [(8, 'simple', 5000, 3), (9, 'efficiency', 20000, 4), (7, 'aggressive', 777, 5),
+                                    (12, 'balanced', 50000, 6)]:
+        eng, st = _run_pair(goal, heur, width, seed)
+        ora = oracle_c.OracleSolve(goal, use_heuristic=True, heuristic_name=heur, beam_width=width, mt_state625=st)
+        t = 0
+        while True:
+            a, b = eng.step(), ora.step()
+            for k in ('n_parents', 'n_raw', 'n_unique', 'n_kept', 'done', 'winner_rank', 'records'):
+                assert a[k] == b[k], (goal, heur, t, k)
+            if a['done']:
+                break
+            t += 1
+            _, _, pa, ka = eng.read_turn(t)
+            _, _, pb, kb = ora.turn_arrays(t)
+            assert np.array_equal(ka, kb) and np.array_equal(pa, pb)
+        assert eng.path() == ora.path()
+        assert np.array_equal(eng.mt_state(), ora.mt_state())
+        eng.close()
+        ora.close()
