@@ -107,6 +107,9 @@ int sb_path(sb_engine* e, uint64_t* lo, uint64_t* hi, int32_t cap, int32_t* len)
  * `random` ends where the reference's would after solve(). */
 int sb_get_mt_state(sb_engine* e, uint32_t* out625);
 
+/* Block until all device work of the handle has finished. */
+int sb_sync(sb_engine* e);
+
 /* Visited-set entries (len(trail)). */
 int sb_visited_size(sb_engine* e, uint64_t* out);
 
@@ -118,8 +121,11 @@ int sb_version(void);
 /* Ordered successors of n parents, stride 192 per parent: out_count[i] children for parent i. */
 int sb_debug_successors(int32_t device, const uint64_t* lo, const uint64_t* hi, int64_t n,
                         uint64_t* out_lo, uint64_t* out_hi, uint64_t* out_key, int32_t* out_count);
-/* n tempered MT19937 words continuing from mt_state625 (device generator). */
+/* n tempered MT19937 words continuing from mt_state625 (device jump-ahead producers: 256 x 1 twist). */
 int sb_debug_mt_words(int32_t device, const uint32_t* mt_state625, int64_t n, uint32_t* out);
+/* same with `producers` (power of two) producers of `twists` twists per segment */
+int sb_debug_mt_words_cfg(int32_t device, const uint32_t* mt_state625, int64_t n, int32_t producers,
+                          int64_t twists, uint32_t* out);
 /* Scores of n states with the given randint values k (1..100). */
 int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const uint64_t* hi,
                     const int32_t* k, int64_t n, double* out);

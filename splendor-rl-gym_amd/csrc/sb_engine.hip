@@ -574,7 +574,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     }
     const bool heur = E.cfg.use_heuristic != 0;
     // speculative noise for this step (side stream, overlaps expansion)
-    if (heur) noise_generate_async(E.noise, (uint64_t)std::max<int64_t>(n * 16, 1 << 20), E.s_mt);
+    if (heur && E.noise.produced - E.noise.consumed < (uint64_t)n * 12) noise_generate_async(E.noise, E.s_mt);
 
     if (timing) SB_HIP(hipEventRecord(E.ev[0], E.s));
     E.desc.ensure((size_t)n * MAX_CHILDREN);
@@ -799,9 +799,14 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         hipLaunchKernelGGL(k_insert_root, dim3(1), dim3(1), 0, E.s, E.tab, E.tab_mask, key_of(root_lo, root_hi));
         SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
         hipLaunchKernelGGL(k_pts_first, dim3(1), dim3(256), 0, E.s, t0.hi, (int64_t)1, E.d_small + 8);
+        // MT chunk = 256 producers x twists x 624 words ~ 16 draws per beam slot; ring >= 4 chunks
+        int64_t twists = 1;
+        while (twists < 512 && (double)twists * 256 * 624 < (double)cfg->beam_width * 16) twists <<= 1;
         uint64_t ring = 1ull << 24;
-        while (ring < (uint64_t)cfg->beam_width * 64 && ring < (1ull << 34)) ring <<= 1;
-        noise_init(E.noise, mt_state625, ring, E.s);
+        while ((ring < (uint64_t)cfg->beam_width * 64 || ring < 4ull * 256 * 624 * (uint64_t)twists) &&
+               ring < (1ull << 35))
+            ring <<= 1;
+        noise_init(E.noise, mt_state625, ring, twists, E.s);
         SB_HIP(hipStreamSynchronize(E.s));
         return SB_OK;
     });
@@ -885,6 +890,7 @@ int sb_path(sb_engine* h, uint64_t* lo, uint64_t* hi, int32_t cap, int32_t* len)
     }
     return guarded([&]() {
         SB_HIP(hipSetDevice(E.dev));
+        SB_HIP(hipStreamSynchronize(E.s));
         int64_t r = E.winner_rank;
         for (int t = T - 1; t >= 0; t--) {
             uint32_t p = 0;
@@ -902,6 +908,16 @@ int sb_get_mt_state(sb_engine* h, uint32_t* out625) {
     if (!h || !out625) return SB_ERR_ARG;
     noise_mt_state(h->E.noise, out625);
     return SB_OK;
+}
+
+int sb_sync(sb_engine* h) {
+    if (!h) return SB_ERR_ARG;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(h->E.dev));
+        SB_HIP(hipStreamSynchronize(h->E.s));
+        SB_HIP(hipStreamSynchronize(h->E.s_mt));
+        return SB_OK;
+    });
 }
 
 int sb_visited_size(sb_engine* h, uint64_t* out) {
@@ -990,10 +1006,15 @@ int sb_debug_successors(int32_t device, const uint64_t* lo, const uint64_t* hi, 
 }
 
 int sb_debug_mt_words(int32_t device, const uint32_t* mt_state625, int64_t n, uint32_t* out) {
-    if (!mt_state625 || !out || n < 0) return SB_ERR_ARG;
+    return sb_debug_mt_words_cfg(device, mt_state625, n, 256, 1, out);
+}
+
+int sb_debug_mt_words_cfg(int32_t device, const uint32_t* mt_state625, int64_t n, int32_t producers,
+                          int64_t twists, uint32_t* out) {
+    if (!mt_state625 || !out || n < 0 || producers < 1 || twists < 1) return SB_ERR_ARG;
     return guarded([&]() {
         SB_HIP(hipSetDevice(device));
-        mt_debug_words(mt_state625, n, out);
+        mt_debug_words(mt_state625, n, producers, twists, out);
         return SB_OK;
     });
 }

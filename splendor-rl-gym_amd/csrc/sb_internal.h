@@ -72,9 +72,21 @@ struct HostMT {
     int idx;
     uint32_t next();
 };
+// P jump-ahead producers; chunk c covers stream words [c*P*L, (c+1)*P*L), L = twists*624
+struct MTProducers {
+    int P = 0;
+    int64_t twists = 0;
+    int64_t chunk = 0;
+    uint32_t* d_win = nullptr;     // P x 624 segment-start windows
+    uint32_t* d_poly = nullptr;    // jump polynomials (doubling tree + chunk stride)
+    uint32_t* chunk_poly = nullptr;
+    void init(const uint32_t origin[624], int P, int64_t twists, hipStream_t st);
+    void gen_chunk(uint32_t* out, hipStream_t st);   // P*L tempered words
+    void release();
+};
 struct NoiseStream {
-    uint32_t* d_state = nullptr;   // 624 words, device generator state (always at a block boundary)
-    DBuf<uint32_t> raw;            // raw tempered words staging
+    MTProducers prod;
+    DBuf<uint32_t> raw;            // raw tempered words staging (one chunk)
     DBuf<uint8_t> ring;            // accepted randint values 1..100
     uint64_t ring_mask = 0;
     uint64_t produced = 0;         // accepted values written so far (host mirror, valid after sync)
@@ -87,16 +99,17 @@ struct NoiseStream {
     ScanScratch scan;
     hipEvent_t ev_ready = nullptr;
     bool pending = false;
-    uint64_t pending_words = 0;
 };
-void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, hipStream_t st);
-// Launch generation of >= `words` raw words + compaction on stream st (asynchronous).
-void noise_generate_async(NoiseStream& ns, uint64_t words, hipStream_t st);
+void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, int64_t twists, hipStream_t st);
+uint64_t noise_chunk_words(const NoiseStream& ns);
+// Launch one chunk of generation + compaction on stream st (asynchronous; no-op if one is pending
+// or the ring lacks room).
+void noise_generate_async(NoiseStream& ns, hipStream_t st);
 // Block until the ring holds >= need unconsumed values (generating more if necessary).
 void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st);
 void noise_free(NoiseStream& ns);
 void noise_mt_state(NoiseStream& ns, uint32_t* out625);
-// debug: raw device words
-void mt_debug_words(const uint32_t* state625, int64_t n, uint32_t* out);
+// debug: raw device words from P producers of `twists` twists per segment
+void mt_debug_words(const uint32_t* state625, int64_t n, int P, int64_t twists, uint32_t* out);
 
 }  // namespace sb

@@ -3,14 +3,19 @@
 // The reference draws one `randint(1, 100)` per scored state (src/solver.py:215,247,260,284),
 // in next_queue order (the order sorted() calls its key).  CPython implements it as MT19937
 // words w with rejection: value = 1 + (w >> 25), redrawing while (w >> 25) >= 100.  The stream is
-// data-independent, so the engine produces it ahead of use:
-//   k_mt_gen      one workgroup runs the MT19937 twist (3 dependent phases of <= 227 words) and
-//                 writes tempered words;
+// data-independent, so the engine produces it ahead of use, in chunks of P*L words:
+//   k_mt_gen_par  P producers (one workgroup each, one per CU) run the MT19937 twist (3 dependent
+//                 phases of <= 227 words) from their own start window; producer p writes words
+//                 [p*L, (p+1)*L) of the chunk;
+//   k_mt_jump     advances producer windows by J words: w(n+J)[j] = XOR_{g_i=1} y_{n+1+i+j} with
+//                 g = x^(J-1) mod phi (sb_gf2.hip); the sequence y is extended in LDS, the
+//                 correlation runs one wave per (64 outputs x poly slice), uniform over poly bits;
 //   k_mt_count/k_mt_write   order-preserving compaction of accepted draws into a ring of u8
 //                 values, so next_queue element k reads ring[(consumed + k) & mask].
 #include <string.h>
 
 #include "sb_block.h"
+#include "sb_gf2.h"
 #include "sb_internal.h"
 
 namespace sb {
@@ -38,29 +43,6 @@ uint32_t HostMT::next() {
         idx = 0;
     }
     return mt_temper(mt[idx++]);
-}
-
-// One workgroup of 640 threads; state in LDS ping-pong buffers; ntw twists.
-__global__ __launch_bounds__(640) void k_mt_gen(uint32_t* __restrict__ state, uint32_t* __restrict__ out, int64_t ntw) {
-    __shared__ uint32_t buf[2][624];
-    const int t = threadIdx.x;
-    if (t < 624) buf[0][t] = state[t];
-    __syncthreads();
-    int cur = 0;
-    for (int64_t w = 0; w < ntw; w++) {
-        uint32_t* A = buf[cur];
-        uint32_t* B = buf[cur ^ 1];
-        if (t < 227) B[t] = mt_mix(A[t], A[t + 1], A[t + 397]);                    // new[i], i < 227
-        __syncthreads();
-        if (t < 227) B[227 + t] = mt_mix(A[227 + t], A[228 + t], B[t]);          // i in [227, 454)
-        __syncthreads();
-        if (t < 169) B[454 + t] = mt_mix(A[454 + t], A[455 + t], B[227 + t]);   // i in [454, 623)
-        else if (t == 169) B[623] = mt_mix(A[623], B[0], B[396]);               // i = 623
-        __syncthreads();
-        if (t < 624) out[w * 624 + t] = mt_temper(B[t]);
-        cur ^= 1;
-    }
-    if (t < 624) state[t] = buf[cur][t];
 }
 
 constexpr int MT_NT = 256;
@@ -105,7 +87,123 @@ __global__ __launch_bounds__(MT_NT) void k_mt_write(const uint32_t* __restrict__
     }
 }
 
-void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, hipStream_t st) {
+// P producers, one workgroup each; producer b runs `twists` twists from window b.
+__global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
+                                                     int64_t twists) {
+    __shared__ uint32_t buf[2][624];
+    const int t = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    if (t < 624) buf[0][t] = wins[b * 624 + t];
+    __syncthreads();
+    uint32_t* o = out + b * twists * 624;
+    int cur = 0;
+    for (int64_t w = 0; w < twists; w++) {
+        uint32_t* A = buf[cur];
+        uint32_t* B = buf[cur ^ 1];
+        if (t < 227) B[t] = mt_mix(A[t], A[t + 1], A[t + 397]);
+        __syncthreads();
+        if (t < 227) B[227 + t] = mt_mix(A[227 + t], A[228 + t], B[t]);
+        __syncthreads();
+        if (t < 169) B[454 + t] = mt_mix(A[454 + t], A[455 + t], B[227 + t]);
+        else if (t == 169) B[623] = mt_mix(A[623], B[0], B[396]);
+        __syncthreads();
+        if (t < 624) o[w * 624 + t] = mt_temper(B[t]);
+        cur ^= 1;
+    }
+}
+
+constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
+constexpr int JMP_NT = 1024;
+constexpr int JMP_PARTS = 8;               // poly split: 8 x 78 words
+constexpr int JMP_JG = 10;                 // 624 outputs in groups of 64
+
+// window src0+b -> window dst0+b advanced by J (gp = x^(J-1) mod phi as 624 u32).  In place is safe.
+__global__ __launch_bounds__(JMP_NT) void k_mt_jump(const uint32_t* win_in, uint32_t* win_out, int src0, int dst0,
+                                                     const uint32_t* __restrict__ gpoly) {
+    __shared__ uint32_t seq[JMP_SEQ + 64];
+    __shared__ uint32_t res[624];
+    __shared__ uint32_t gp[624];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int64_t src = src0 + blockIdx.x, dst = dst0 + blockIdx.x;
+    for (int i = t; i < 624; i += JMP_NT) {
+        seq[i] = win_in[src * 624 + i];
+        res[i] = 0;
+        gp[i] = gpoly[i];
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < JMP_SEQ - 624; k0 += 227) {   // y_{k+624} = f(y_k, y_{k+1}, y_{k+397})
+        const int k = k0 + t;
+        if (t < 227 && k < JMP_SEQ - 624) seq[k + 624] = mt_mix(seq[k], seq[k + 1], seq[k + 397]);
+        __syncthreads();
+    }
+    for (int task = w; task < JMP_JG * JMP_PARTS; task += JMP_NT / 64) {
+        const int jg = task % JMP_JG, part = task / JMP_JG;
+        const int j = jg * 64 + lane;
+        const int jj = j < 624 ? j : 623;
+        uint32_t acc = 0;
+        const int w0 = part * (624 / JMP_PARTS), w1 = w0 + 624 / JMP_PARTS;
+        for (int wi = w0; wi < w1; wi++) {
+            uint32_t bits = gp[wi];   // wave-uniform
+            while (bits) {
+                const int b = __builtin_ctz(bits);
+                bits &= bits - 1;
+                acc ^= seq[1 + wi * 32 + b + jj];
+            }
+        }
+        if (j < 624) atomicXor(&res[j], acc);
+    }
+    __syncthreads();
+    for (int i = t; i < 624; i += JMP_NT) win_out[dst * 624 + i] = res[i];
+}
+
+void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipStream_t st) {
+    if (P_ < 1 || (P_ & (P_ - 1))) throw HipError{hipErrorInvalidValue, "MT producers must be a power of two"};
+    if (!gf2::self_test()) throw HipError{hipErrorInvalidValue, "MT19937 jump-ahead self-test failed"};
+    P = P_;
+    twists = twists_;
+    chunk = 0;
+    const uint64_t L = (uint64_t)twists * 624;
+    int levels = 0;
+    while ((1 << levels) < P) levels++;
+    std::vector<uint32_t> polys((size_t)(levels + 1) * 624);
+    for (int k = 0; k < levels; k++) gf2::to_words(gf2::jump_poly(L << k), &polys[(size_t)k * 624]);
+    gf2::to_words(gf2::jump_poly(L * (uint64_t)P), &polys[(size_t)levels * 624]);
+    SB_HIP(hipMalloc((void**)&d_win, (size_t)P * 624 * 4));
+    SB_HIP(hipMalloc((void**)&d_poly, polys.size() * 4));
+    SB_HIP(hipMemcpyAsync(d_poly, polys.data(), polys.size() * 4, hipMemcpyHostToDevice, st));
+    SB_HIP(hipMemcpyAsync(d_win, origin, 624 * 4, hipMemcpyHostToDevice, st));
+    for (int k = 0; k < levels; k++)   // doubling tree: windows [2^k, 2^(k+1)) from [0, 2^k)
+        hipLaunchKernelGGL(k_mt_jump, dim3(1u << k), dim3(JMP_NT), 0, st, d_win, d_win, 0, 1 << k,
+                           d_poly + (size_t)k * 624);
+    chunk_poly = d_poly + (size_t)levels * 624;
+    SB_HIP(hipGetLastError());
+}
+
+void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
+    if (chunk > 0)   // every producer jumps P*L ahead of its previous segment start
+        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
+    hipLaunchKernelGGL(k_mt_gen_par, dim3(P), dim3(640), 0, st, d_win, out, twists);
+    SB_HIP(hipGetLastError());
+    chunk++;
+}
+
+void MTProducers::release() {
+    if (d_win) (void)hipFree(d_win);
+    if (d_poly) (void)hipFree(d_poly);
+    d_win = d_poly = nullptr;
+}
+
+static void compact_accepted(NoiseStream& ns, const uint32_t* raw, int64_t n, hipStream_t st) {
+    int64_t nt = (n + MT_TILE - 1) / MT_TILE;
+    ns.scan.tiles.ensure(nt);
+    hipLaunchKernelGGL(k_mt_count, dim3((unsigned)nt), dim3(MT_NT), 0, st, raw, n, ns.scan.tiles.p);
+    scan_tiles_inplace(ns.scan.tiles.p, nt, ns.d_total, st);
+    hipLaunchKernelGGL(k_mt_write, dim3((unsigned)nt), dim3(MT_NT), 0, st, raw, n, ns.scan.tiles.p, ns.ring.p,
+                       ns.ring_mask, ns.produced);
+    SB_HIP(hipMemcpyAsync(ns.h_total, ns.d_total, 4, hipMemcpyDeviceToHost, st));
+}
+
+void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, int64_t twists, hipStream_t st) {
     memcpy(ns.initial.mt, state625, 624 * 4);
     ns.initial.idx = (int)state625[624];
     ns.replay = ns.initial;
@@ -114,53 +212,37 @@ void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow
     ns.consumed = 0;
     ns.ring.ensure(ring_cap_pow2);
     ns.ring_mask = ring_cap_pow2 - 1;
-    SB_HIP(hipMalloc((void**)&ns.d_state, 624 * 4));
     SB_HIP(hipMalloc((void**)&ns.d_total, 16));
     SB_HIP(hipHostMalloc((void**)&ns.h_total, 16, hipHostMallocDefault));
     SB_HIP(hipEventCreateWithFlags(&ns.ev_ready, hipEventDisableTiming));
-    // the host emits the partially consumed block (words idx..623) so the device always starts
-    // with a twist; those words go through the same compaction
+    // the host emits the partially consumed block (words idx..623); the device producers start at
+    // the next twist of the remaining window
     HostMT h = ns.initial;
     uint32_t lead[624];
     int nlead = 0;
     while (h.idx < 624) lead[nlead++] = h.next();
-    SB_HIP(hipMemcpyAsync(ns.d_state, h.mt, 624 * 4, hipMemcpyHostToDevice, st));
+    ns.prod.init(h.mt, 256, twists, st);
     if (nlead) {
         ns.raw.ensure(624);
         SB_HIP(hipMemcpyAsync(ns.raw.p, lead, nlead * 4, hipMemcpyHostToDevice, st));
-        int64_t nt = (nlead + MT_TILE - 1) / MT_TILE;
-        ns.scan.tiles.ensure(nt);
-        hipLaunchKernelGGL(k_mt_count, dim3((unsigned)nt), dim3(MT_NT), 0, st, ns.raw.p, (int64_t)nlead, ns.scan.tiles.p);
-        scan_tiles_inplace(ns.scan.tiles.p, nt, ns.d_total, st);
-        hipLaunchKernelGGL(k_mt_write, dim3((unsigned)nt), dim3(MT_NT), 0, st, ns.raw.p, (int64_t)nlead, ns.scan.tiles.p,
-                           ns.ring.p, ns.ring_mask, (uint64_t)0);
-        SB_HIP(hipMemcpyAsync(ns.h_total, ns.d_total, 4, hipMemcpyDeviceToHost, st));
+        compact_accepted(ns, ns.raw.p, nlead, st);
         SB_HIP(hipStreamSynchronize(st));
         ns.produced += *ns.h_total;
     }
 }
 
-void noise_generate_async(NoiseStream& ns, uint64_t words, hipStream_t st) {
+uint64_t noise_chunk_words(const NoiseStream& ns) { return (uint64_t)ns.prod.P * ns.prod.twists * 624; }
+
+void noise_generate_async(NoiseStream& ns, hipStream_t st) {
     if (ns.pending) return;
-    uint64_t room = ns.ring_mask + 1 - (ns.produced - ns.consumed);
-    // never let unconsumed values overrun the ring: accepted draws <= words generated
-    if (words > room) words = room;
-    int64_t ntw = (int64_t)(words / 624);
-    if (ntw <= 0) return;
-    int64_t n = ntw * 624;
+    const uint64_t n = noise_chunk_words(ns);
+    const uint64_t room = ns.ring_mask + 1 - (ns.produced - ns.consumed);
+    if (n > room) return;   // accepted draws <= words: never overrun unconsumed values
     ns.raw.ensure((size_t)n);
-    hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, st, ns.d_state, ns.raw.p, ntw);
-    int64_t nt = (n + MT_TILE - 1) / MT_TILE;
-    ns.scan.tiles.ensure(nt);
-    hipLaunchKernelGGL(k_mt_count, dim3((unsigned)nt), dim3(MT_NT), 0, st, ns.raw.p, n, ns.scan.tiles.p);
-    scan_tiles_inplace(ns.scan.tiles.p, nt, ns.d_total, st);
-    hipLaunchKernelGGL(k_mt_write, dim3((unsigned)nt), dim3(MT_NT), 0, st, ns.raw.p, n, ns.scan.tiles.p, ns.ring.p,
-                       ns.ring_mask, ns.produced);
-    SB_HIP(hipMemcpyAsync(ns.h_total, ns.d_total, 4, hipMemcpyDeviceToHost, st));
+    ns.prod.gen_chunk(ns.raw.p, st);
+    compact_accepted(ns, ns.raw.p, (int64_t)n, st);
     SB_HIP(hipEventRecord(ns.ev_ready, st));
-    SB_HIP(hipGetLastError());
     ns.pending = true;
-    ns.pending_words = (uint64_t)n;
 }
 
 static void noise_collect(NoiseStream& ns) {
@@ -172,11 +254,10 @@ static void noise_collect(NoiseStream& ns) {
 
 void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st) {
     noise_collect(ns);
+    if (need > ns.ring_mask + 1 - noise_chunk_words(ns))
+        throw HipError{hipErrorOutOfMemory, "noise ring too small for one step"};
     while (ns.produced - ns.consumed < need) {
-        uint64_t deficit = need - (ns.produced - ns.consumed);
-        if (deficit > ns.ring_mask + 1) throw HipError{hipErrorOutOfMemory, "noise ring too small for one step"};
-        uint64_t words = deficit * 128 / 100 + 8192;
-        noise_generate_async(ns, words, st);
+        noise_generate_async(ns, st);
         if (!ns.pending) throw HipError{hipErrorOutOfMemory, "noise ring full"};
         noise_collect(ns);
     }
@@ -194,37 +275,38 @@ void noise_mt_state(NoiseStream& ns, uint32_t* out625) {
 }
 
 void noise_free(NoiseStream& ns) {
-    if (ns.d_state) (void)hipFree(ns.d_state);
     if (ns.d_total) (void)hipFree(ns.d_total);
     if (ns.h_total) (void)hipHostFree(ns.h_total);
     if (ns.ev_ready) (void)hipEventDestroy(ns.ev_ready);
+    ns.prod.release();
     ns.raw.release();
     ns.ring.release();
     ns.scan.tiles.release();
-    ns.d_state = nullptr;
     ns.d_total = nullptr;
     ns.h_total = nullptr;
     ns.ev_ready = nullptr;
 }
 
-void mt_debug_words(const uint32_t* state625, int64_t n, uint32_t* out) {
+void mt_debug_words(const uint32_t* state625, int64_t n, int P, int64_t twists, uint32_t* out) {
     HostMT h;
     memcpy(h.mt, state625, 624 * 4);
     h.idx = (int)state625[624];
     int64_t k = 0;
     while (h.idx < 624 && k < n) out[k++] = h.next();
     if (k == n) return;
-    int64_t ntw = (n - k + 623) / 624;
-    uint32_t* ds = nullptr;
+    MTProducers prod;
+    prod.init(h.mt, P, twists, 0);
+    const int64_t cw = (int64_t)P * twists * 624;
     uint32_t* dout = nullptr;
-    SB_HIP(hipMalloc((void**)&ds, 624 * 4));
-    SB_HIP(hipMalloc((void**)&dout, (size_t)ntw * 624 * 4));
-    SB_HIP(hipMemcpy(ds, h.mt, 624 * 4, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_mt_gen, dim3(1), dim3(640), 0, 0, ds, dout, ntw);
-    SB_HIP(hipGetLastError());
-    SB_HIP(hipMemcpy(out + k, dout, (size_t)(n - k) * 4, hipMemcpyDeviceToHost));
-    (void)hipFree(ds);
+    SB_HIP(hipMalloc((void**)&dout, (size_t)cw * 4));
+    while (k < n) {
+        prod.gen_chunk(dout, 0);
+        const int64_t take = n - k < cw ? n - k : cw;
+        SB_HIP(hipMemcpy(out + k, dout, (size_t)take * 4, hipMemcpyDeviceToHost));
+        k += take;
+    }
     (void)hipFree(dout);
+    prod.release();
 }
 
 }  // namespace sb

@@ -15,7 +15,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(PKG_DIR), 'csrc')
 LIB_PATH = os.path.join(PKG_DIR, 'libsplendor_beam.so')
-SOURCES = ['sb_engine.hip', 'sb_scan.hip', 'sb_sort.hip', 'sb_mt.hip']
+SOURCES = ['sb_engine.hip', 'sb_scan.hip', 'sb_sort.hip', 'sb_mt.hip', 'sb_gf2.hip']
 
 SB_OK = 0
 SB_ERR_ARG = -1
@@ -28,8 +28,8 @@ SB_ERR_NOTABLES = -5
 POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
 EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
-            'sb_get_mt_state', 'sb_visited_size', 'sb_destroy', 'sb_last_error', 'sb_version',
-            'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_scores', 'sb_debug_topk')
+            'sb_get_mt_state', 'sb_sync', 'sb_visited_size', 'sb_destroy', 'sb_last_error', 'sb_version',
+            'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk')
 
 
 class SplendorBeamError(RuntimeError):
@@ -104,11 +104,13 @@ def lib():
         L.sb_path.argtypes = [vp, u64p, u64p, C.c_int32, C.POINTER(C.c_int32)]
         L.sb_get_mt_state.argtypes = [vp, u32p]
         L.sb_visited_size.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.sb_sync.argtypes = [vp]
         L.sb_destroy.argtypes = [vp]
         L.sb_destroy.restype = None
         L.sb_last_error.restype = C.c_char_p
         L.sb_debug_successors.argtypes = [C.c_int32, u64p, u64p, C.c_int64, u64p, u64p, u64p, i32p]
         L.sb_debug_mt_words.argtypes = [C.c_int32, u32p, C.c_int64, u32p]
+        L.sb_debug_mt_words_cfg.argtypes = [C.c_int32, u32p, C.c_int64, C.c_int32, C.c_int64, u32p]
         L.sb_debug_scores.argtypes = [C.c_int32, C.c_int32, u64p, u64p, i32p, C.c_int64, f64p]
         L.sb_debug_topk.argtypes = [C.c_int32, u64p, C.c_int64, C.c_int64, u32p]
         _lib = L

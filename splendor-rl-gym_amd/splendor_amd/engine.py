@@ -93,6 +93,9 @@ class BeamEngine:
         L.check(L.lib().sb_get_mt_state(self._h, out), 'sb_get_mt_state')
         return out
 
+    def sync(self):
+        L.check(L.lib().sb_sync(self._h), 'sb_sync')
+
     def visited_size(self) -> int:
         v = C.c_uint64()
         L.check(L.lib().sb_visited_size(self._h, C.byref(v)))
@@ -114,9 +117,15 @@ def device_successors(lo, hi, device: int = 0):
             for i in range(n)]
 
 
-def device_mt_words(state625, n: int, device: int = 0) -> np.ndarray:
+def device_mt_words(state625, n: int, device: int = 0, producers: int | None = None,
+                    twists: int = 1) -> np.ndarray:
+    """Tempered MT19937 words from the device jump-ahead producers (continuing from state625)."""
     out = np.zeros(n, np.uint32)
-    L.check(L.lib().sb_debug_mt_words(device, np.ascontiguousarray(np.array(state625, np.uint32)), n, out))
+    st = np.ascontiguousarray(np.array(state625, np.uint32))
+    if producers is None:
+        L.check(L.lib().sb_debug_mt_words(device, st, n, out), 'sb_debug_mt_words')
+    else:
+        L.check(L.lib().sb_debug_mt_words_cfg(device, st, n, producers, twists, out), 'sb_debug_mt_words_cfg')
     return out
 
 

@@ -73,6 +73,20 @@ def test_device_mt_words(tables):
     assert np.array_equal(w, ref)
 
 
+@pytest.mark.parametrize('producers,twists,n', [(1, 1, 5000), (4, 3, 50_000), (8, 1, 31_000), (256, 2, 400_000),
+                                                (256, 64, 25_000_000)])
+def test_device_mt_jump_ahead(producers, twists, n):
+    """Jump-ahead producers (doubling tree + chunk stride) reproduce the sequential stream word for word."""
+    random.seed(producers * 1000 + twists)
+    for _ in range(17):
+        random.getrandbits(32)
+    st = random.getstate()[1]
+    w = device_mt_words(st, n, producers=producers, twists=twists)
+    ref = np.zeros(n, np.uint32)
+    oracle_c.lib().oc_mt_words(np.array(st, np.uint32), ref, n)
+    assert np.array_equal(w, ref)
+
+
 @pytest.mark.parametrize('hid,name', [(0, 'simple'), (1, 'balanced'), (2, 'aggressive'), (3, 'efficiency'),
                                       (1, 'competitive')])
 def test_device_scores_golden(tables, hid, name):
