@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Summarise a profiles/collect.sh run: per-kernel device time of the timed steps (kernel trace) and
+HBM traffic per launch from the PMC passes.
+
+Timed steps = the last `--steps` dispatches of each per-step kernel (bench.py runs setup turns,
+warmup, then the timed steps).  Traffic per the guide (MI355X_MICROARCH.md §HBM; cdna_hip_programming
+§7): FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide
+coalesced stream, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (the x2 is calibrated for
+16 B/lane streams; other widths uncalibrated — stated beside the number).
+"""
+import argparse
+import csv
+import json
+import os
+import re
+from collections import defaultdict
+
+PER_STEP = ['k_expand', 'k_survive', 'k_emit<', 'k_gather', 'k_sel_write', 'k_sel_count']
+
+
+def short(name):
+    m = re.match(r'(?:void )?(?:sb::)?([A-Za-z_0-9]+(?:<\d+>)?)', name)
+    return m.group(1) if m else name[:40]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('dir')
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--out', required=True)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(os.path.join(a.dir, 'trace', 'run_kernel_trace.csv'))))
+    by = defaultdict(list)
+    for r in rows:
+        by[short(r['Kernel_Name'])].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+    kernels = {}
+    for k, durs in by.items():
+        kernels[k] = {'calls': len(durs), 'total_ns': sum(durs), 'avg_ns': sum(durs) / len(durs)}
+    # timed-step view of the per-step kernels
+    timed = {}
+    for k in ('k_expand', 'k_survive', 'k_emit<1>', 'k_gather'):
+        if k in by:
+            d = by[k][-a.steps:]
+            timed[k] = {'launches': len(d), 'avg_ns': sum(d) / len(d)}
+    pmc = {}
+    for kind, fn in (('FETCH_SIZE', 'pmc_fetch'), ('WRITE_SIZE', 'pmc_write')):
+        p = os.path.join(a.dir, fn, 'run_counter_collection.csv')
+        if not os.path.exists(p):
+            continue
+        vals = defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            if r['Counter_Name'] == kind:
+                vals[short(r['Kernel_Name'])].append(float(r['Counter_Value']))
+        for k, v in vals.items():
+            pmc.setdefault(k, {})[kind + '_KiB_timed_avg'] = sum(v[-a.steps:]) / len(v[-a.steps:])
+    for k, v in pmc.items():
+        if 'FETCH_SIZE_KiB_timed_avg' in v and 'WRITE_SIZE_KiB_timed_avg' in v:
+            v['hbm_bytes_per_launch'] = (2 * v['FETCH_SIZE_KiB_timed_avg'] + v['WRITE_SIZE_KiB_timed_avg']) * 1024
+    bench = None
+    bp = os.path.join(a.dir, 'bench_trace.json')
+    if os.path.exists(bp):
+        try:
+            bench = json.loads(open(bp).read().strip().splitlines()[-1])
+        except Exception:
+            bench = None
+    out = {'source': a.dir, 'timed_steps': a.steps, 'timed': timed, 'pmc': pmc,
+           'all_kernels': dict(sorted(kernels.items(), key=lambda kv: -kv[1]['total_ns'])), 'bench': bench}
+    with open(a.out, 'w') as f:
+        json.dump(out, f, indent=1)
+    for k, v in timed.items():
+        t = pmc.get(k, {}).get('hbm_bytes_per_launch')
+        print(f'{k:12s} avg {v["avg_ns"]/1e6:8.3f} ms   hbm/launch {t/1e9 if t else float("nan"):8.3f} GB')
+
+
+if __name__ == '__main__':
+    main()

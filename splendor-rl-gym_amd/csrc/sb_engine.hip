@@ -708,7 +708,7 @@ int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const dou
         set_error("sb_init_tables: null argument");
         return SB_ERR_ARG;
     }
-    Tables& T = g_host_tables;
+    static Tables T;   // validated copy; published to g_host_tables only on success
     memset(&T, 0, sizeof T);
     for (int c = 0; c < NCARDS; c++) {
         const int32_t* r = deck_rows + c * 7;
@@ -734,6 +734,7 @@ int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const dou
     memcpy(T.pw, pow_tables, sizeof T.pw);
     memcpy(T.noise, noise, sizeof T.noise);
     (void)npat_host;
+    g_host_tables = T;
     g_tables_ready = true;
     return SB_OK;
 }

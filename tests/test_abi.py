@@ -1,0 +1,60 @@
+"""The C-ABI library builds for gfx950, loads without a GPU and exports every symbol the header declares."""
+import ctypes
+import os
+import re
+import subprocess
+
+from conftest import REPO
+from splendor_amd import _lib
+
+HEADER = os.path.join(REPO, 'include', 'splendor_beam.h')
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:int|void|const char\*)\s+(sb_\w+)\s*\(', text, re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    assert set(_lib.EXPORTED) == set(syms), set(_lib.EXPORTED) ^ set(syms)
+
+
+def test_library_loads_and_exports_all_symbols():
+    L = _lib.lib()
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+    assert L.sb_version() >= 1
+    out = subprocess.run(['nm', '-D', '--defined-only', _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for s in declared_symbols():
+        assert re.search(rf'\bT {s}$', out, re.M), s
+
+
+def test_library_targets_gfx950():
+    out = subprocess.run(['strings', _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert 'gfx950' in out
+
+
+def test_argument_errors_without_gpu():
+    """Null handles/args are rejected with an error code before any device work."""
+    L = _lib.lib()
+    assert L.sb_step(None, None) == _lib.SB_ERR_ARG
+    assert L.sb_sync(None) == _lib.SB_ERR_ARG
+    cfg = _lib.SbConfig(goal_pts=3, use_heuristic=0, heuristic=0, device=0, beam_width=0)
+    import numpy as np
+    h = ctypes.c_void_p()
+    _lib.ensure_tables()
+    rc = L.sb_create(ctypes.byref(cfg), np.zeros(625, np.uint32), 0, 0, ctypes.byref(h))
+    assert rc == _lib.SB_ERR_ARG
+    assert b'beam_width' in L.sb_last_error()
+
+
+def test_init_tables_validates_deck():
+    import numpy as np
+    L = _lib.lib()
+    bad = np.zeros(90 * 7, np.int32)
+    bad[0] = 9
+    rc = L.sb_init_tables(bad, np.zeros(11 * 256), np.zeros(100))
+    assert rc == _lib.SB_ERR_ARG
+    _lib._tables_ready = False
+    _lib.ensure_tables()

@@ -1,0 +1,109 @@
+"""Host-side logic (no GPU): deck data, state codec, Python heuristics, pow tables, State API."""
+import random
+
+import numpy as np
+import pytest
+
+from splendor_amd import _lib, codec
+from splendor_amd.deck import Color, get_deck
+from splendor_amd.solver import (HEURISTICS, State, aggressive_heuristic, balanced_heuristic,
+                                 efficiency_heuristic, simple_heuristic)
+
+
+def test_deck_matches_reference(tables):
+    deck = get_deck()
+    assert len(deck) == 90
+    for c, g in zip(deck, tables['deck']):
+        assert list(c.cost) == g['cost'] and c.pt == g['pt'] and c.bonus.value == g['color']
+        assert c.str_id == g['str_id']
+
+
+def test_codec_roundtrip_and_hash(tables):
+    for cards, gems, h in tables['hash_vectors'][:500]:
+        lo, hi = codec.encode(cards, gems, 7, 123)
+        c2, _, g2, p2, s2 = codec.decode(lo, hi)
+        assert list(c2) == cards and list(g2) == gems and (p2, s2) == (7, 123)
+        assert codec.to_signed(codec.state_key(tuple(cards), tuple(gems))) == h == hash((tuple(cards), tuple(gems)))
+
+
+def test_codec_rejects_out_of_range():
+    with pytest.raises(ValueError):
+        codec.encode((), (8, 0, 0, 0, 0), 0, 0)
+    with pytest.raises(ValueError):
+        codec.encode((), (0, 0, 0, 0, 0), 0, 1 << 15)
+
+
+def test_pow_and_noise_tables_match_reference(tables):
+    t = _lib.pow_tables()
+    for r, e in enumerate(_lib.POW_EXPONENTS):
+        assert [float(x).hex() for x in t[r]] == tables['pow_tables'][repr(e)]
+    assert [float(x).hex() for x in _lib.noise_table()] == tables['noise_table']
+
+
+@pytest.mark.parametrize('name', ['simple', 'balanced', 'aggressive', 'efficiency', 'competitive'])
+def test_python_heuristics_match_reference(tables, name):
+    for r in tables['heuristic_scores_seed11']:
+        st = State(tuple(r['cards']), tuple(r['bonus']), tuple(r['gems']), r['pts'], r['saved'])
+        random.seed(11)
+        assert HEURISTICS[name](st).hex() == r[name]
+
+
+def test_state_repr(tables):
+    for cards, gems, rep in tables['repr']:
+        lo, hi = codec.encode(cards, gems, 0, 0)
+        assert repr(State.from_packed(lo, hi)) == rep
+    assert repr(State.newgame()) == '(0, 0, 0, 0, 0)'
+
+
+def test_buy_card_sequence():
+    """tests/test_solver.py:23-52 of the reference."""
+    st = State.newgame()
+    st.gems = (4, 3, 0, 7, 2)
+    st = st.buy_card(50)
+    assert st == State(cards=(50,), bonus=(1, 0, 0, 0, 0), gems=(4, 3, 0, 2, 2), pts=2, saved=0)
+    assert (st.gems, st.bonus, st.pts, st.saved) == ((4, 3, 0, 2, 2), (1, 0, 0, 0, 0), 2, 0)
+    st = st.buy_card(6)
+    assert (st.cards, st.gems, st.bonus, st.pts, st.saved) == ((6, 50), (4, 3, 0, 2, 0), (1, 1, 0, 0, 0), 2, 1)
+    st = st.buy_card(57)
+    assert (st.cards, st.gems, st.bonus, st.pts, st.saved) == ((6, 50, 57), (1, 2, 0, 2, 0), (1, 1, 1, 0, 0), 4, 3)
+
+
+def test_state1_fixture_repr():
+    st = State.newgame()
+    for card in (40, 5, 21):
+        st = st.buy_card(card)
+    st.gems = (1, 2, 0, 0, 3)
+    assert st.bonus == (2, 1, 0, 0, 0)
+    assert st.cards == (5, 21, 40)
+    assert repr(st) == '(1, 2, 0, 0, 3) 0W12-0B113-1W223'
+
+
+def test_heuristic_properties():
+    """Registry and monotonicity properties of tests/test_heuristics.py (reference)."""
+    for k in ('simple', 'balanced', 'aggressive', 'efficiency'):
+        assert k in HEURISTICS
+    for h in (simple_heuristic, balanced_heuristic, aggressive_heuristic, efficiency_heuristic):
+        s = h(State.newgame())
+        assert isinstance(s, float) and s >= 0
+    low = State((), (0,) * 5, (0,) * 5, 2, 5)
+    high = State((), (0,) * 5, (0,) * 5, 12, 5)
+    for name, h in HEURISTICS.items():
+        if name == 'competitive':
+            continue
+        assert sum(h(high) for _ in range(10)) > sum(h(low) for _ in range(10))
+    st = State((), (1,) * 5, (3,) * 5, 7, 12)
+    for h in HEURISTICS.values():
+        v = [h(st) for _ in range(10)]
+        assert max(v) - min(v) < 1.0
+
+
+def test_color_enum():
+    assert [c.value for c in Color] == [0, 1, 2, 3, 4]
+    assert repr(Color.RED) == str(Color.RED)
+
+
+def test_custom_heuristic_fails_loudly(monkeypatch):
+    """User Python heuristics cannot run in the device scorer: the solve raises instead of degrading."""
+    monkeypatch.setitem(HEURISTICS, 'mine', lambda s: 1.0)
+    with pytest.raises(NotImplementedError):
+        State.newgame().solve(goal_pts=3, use_heuristic=True, heuristic_name='mine', verbose=False)
