@@ -157,6 +157,14 @@ def test_solve_w300k_golden(name):
     _check_against_golden(golden(name))
 
 
+def test_solve_c3_w4m_oracle_golden():
+    """Config C3 (goal 15 -u -H balanced W=4M seed 0): the reference cannot run it here (RAM), so the
+    golden is the C oracle's (itself pinned to the reference's W<=300k captures)."""
+    g = golden('oracle_g15_balanced_w4000000_s0.json')
+    assert g['moves'] == 15
+    _check_against_golden(g)
+
+
 def test_bfs_golden():
     for g in golden('bfs.json'):
         eng = BeamEngine(goal_pts=g['goal'], use_heuristic=False, heuristic=0, beam_width=1, mt_state625=_mt(0))
