@@ -132,6 +132,37 @@ int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const
 /* Stable descending sort of n u64 keys: out_idx = permutation (ties keep input order), first `keep`. */
 int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx);
 
+/* ---- sharded mode (cfg.world_size > 1): per-rank step primitives; the exchanges between them are
+ * the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers are caller-owned
+ * buffers on the engine's device; every call returns after its device work has completed. ---- */
+/* local first rank per pts of this rank's queue slice (0xFFFFFFFF = none) */
+int sbd_goal_table(sb_engine* e, uint32_t* first256);
+/* expand the local slice (global queue offset goff), drop children this rank generated before or
+ * earlier this turn; owner_counts[world] = records per owner rank, *n_raw = successors generated */
+int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int64_t* owner_counts, int64_t* n_raw);
+/* candidate records grouped by owner (rank, ordinal order inside a group): key, global tag */
+int sbd_pack(sb_engine* e, uint64_t* d_key, uint64_t* d_tag);
+/* owner side: claim n received records in this rank's trail shard; d_ret[i] = 1 if first occurrence */
+int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, const uint64_t* d_tag, int64_t n, uint8_t* d_ret);
+/* apply the answers (in pack order); *n_unique_local = this rank's next_queue entries */
+int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
+/* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */
+int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
+/* radix-select pass: histogram of the next 8 bits of keys whose top `bits` bits equal pref[j] */
+int sbd_hist(sb_engine* e, int32_t nb, const uint64_t* pref_host, int32_t bits, int64_t* hist_host);
+int sbd_eq_count(sb_engine* e, uint64_t T, int64_t* out);
+/* kept = key > T or (key == T and local tie index < quota) [if has_top]; destination range =
+ * #{j : key < split_j}; dest_counts[world] */
+int sbd_partition(sb_engine* e, int32_t has_top, uint64_t T, int64_t quota, int32_t nsplit,
+                  const uint64_t* splits_host, int32_t world, int64_t* dest_counts);
+int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, int64_t* dest_counts);
+/* kept records grouped by destination, next_queue order inside a group */
+int sbd_pack_kept(sb_engine* e, uint64_t* d_lo, uint64_t* d_hi, uint64_t* d_par, uint64_t* d_key);
+/* the new slice: received records (global next_queue order), stable-sorted by score if heur */
+int sbd_receive(sb_engine* e, const uint64_t* d_lo, const uint64_t* d_hi, const uint64_t* d_par,
+                const uint64_t* d_key, int64_t n, int32_t heur);
+int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
+
 #ifdef __cplusplus
 }
 #endif

@@ -283,7 +283,8 @@ __global__ __launch_bounds__(256) void k_emit(const Tables* __restrict__ T, cons
                                               const uint32_t* __restrict__ off, uint64_t* __restrict__ nlo,
                                               uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
                                               uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
-                                              uint64_t ring_mask, uint64_t ring_base, uint32_t* __restrict__ err) {
+                                              uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
+                                              uint32_t* __restrict__ err) {
     __shared__ uint32_t card[NCARDS];
     __shared__ uint32_t pat[4][NPAT_MAX];
     __shared__ int32_t npat[4];
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(256) void k_emit(const Tables* __restrict__ T, cons
                 }
                 nlo[kk] = clo;
                 nhi[kk] = chi;
-                npar[kk] = (uint32_t)r;
+                npar[kk] = par_base + (uint32_t)r;
                 if constexpr (H >= 0) {
                     if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
                     const int nv = ring[(ring_base + kk) & ring_mask];
@@ -503,6 +504,15 @@ struct Engine {
     int64_t winner_rank = -1;
     int max_pts = 0;
     hipEvent_t ev[8] = {};
+    // distributed mode (world_size > 1): owner shard of the global visited set + exchange staging
+    Entry* own = nullptr;
+    uint64_t own_mask = 0;
+    int64_t ncand = 0, nuniq_local = 0, nkept_local = 0;
+    int64_t goff = 0;
+    int part_D = 1;
+    DBuf<uint64_t> cand_key, cand_tag;
+    DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
+    DBuf<uint8_t> digit;
 };
 
 static void check_err_word(Engine& E) {
@@ -625,13 +635,13 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     if (!heur) {
         hipLaunchKernelGGL(k_emit<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p,
                            E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,
-                           E.d_small + 1);
+                           0u, E.d_small + 1);
     } else {
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                     \
     hipLaunchKernelGGL(k_emit<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p, \
                        E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,    \
-                       E.d_small + 1);                                                                              \
+                       0u, E.d_small + 1);                                                                          \
     break;
             case 1: EMIT(1)
             case 2: EMIT(2)
@@ -781,6 +791,14 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         E.tab_mask = cap - 1;
         SB_HIP(hipMalloc((void**)&E.tab, cap * sizeof(Entry)));
         SB_HIP(hipMemsetAsync(E.tab, 0xFF, cap * sizeof(Entry), E.s));
+        const bool distm = cfg->world_size > 1;
+        if (distm) {
+            if (cfg->rank < 0 || cfg->rank >= cfg->world_size || cfg->world_size > 64)
+                throw HipError{hipErrorInvalidValue, "bad rank / world_size (<= 64)"};
+            E.own_mask = cap - 1;
+            SB_HIP(hipMalloc((void**)&E.own, cap * sizeof(Entry)));
+            SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
+        }
         SB_HIP(hipMalloc((void**)&E.d_small, 264 * 4));
         SB_HIP(hipMalloc((void**)&E.d_nraw, 8));
         SB_HIP(hipHostMalloc((void**)&E.h_small, 264 * 4, hipHostMallocDefault));
@@ -795,11 +813,12 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         SB_HIP(hipMemcpyAsync(t0.lo, &root_lo, 8, hipMemcpyHostToDevice, E.s));
         SB_HIP(hipMemcpyAsync(t0.hi, &root_hi, 8, hipMemcpyHostToDevice, E.s));
         SB_HIP(hipMemcpyAsync(t0.par, &nopar, 4, hipMemcpyHostToDevice, E.s));
-        t0.n = 1;
+        t0.n = (!distm || cfg->rank == 0) ? 1 : 0;   // sharded: the root is global rank 0, held by rank 0
         E.turns.push_back(t0);
         hipLaunchKernelGGL(k_insert_root, dim3(1), dim3(1), 0, E.s, E.tab, E.tab_mask, key_of(root_lo, root_hi));
+        if (distm) hipLaunchKernelGGL(k_insert_root, dim3(1), dim3(1), 0, E.s, E.own, E.own_mask, key_of(root_lo, root_hi));
         SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
-        hipLaunchKernelGGL(k_pts_first, dim3(1), dim3(256), 0, E.s, t0.hi, (int64_t)1, E.d_small + 8);
+        hipLaunchKernelGGL(k_pts_first, dim3(1), dim3(256), 0, E.s, t0.hi, t0.n, E.d_small + 8);
         // MT chunk = 256 producers x twists x 624 words ~ 16 draws per beam slot; ring >= 4 chunks
         int64_t twists = 1;
         while (twists < 512 && (double)twists * 256 * 624 < (double)cfg->beam_width * 16) twists <<= 1;
@@ -962,6 +981,14 @@ void sb_destroy(sb_engine* h) {
     if (E.topk.h_flags) (void)hipHostFree(E.topk.h_flags);
     noise_free(E.noise);
     if (E.tab) (void)hipFree(E.tab);
+    if (E.own) (void)hipFree(E.own);
+    E.cand_key.release();
+    E.cand_tag.release();
+    E.cand_ro.release();
+    E.cand_pos.release();
+    E.own_slot.release();
+    E.part_hist.release();
+    E.digit.release();
     if (E.d_tables) (void)hipFree(E.d_tables);
     if (E.d_small) (void)hipFree(E.d_small);
     if (E.d_nraw) (void)hipFree(E.d_nraw);
@@ -1094,3 +1121,5 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
 }
 
 }  // extern "C"
+
+#include "sb_dist.inc"

@@ -29,7 +29,9 @@ POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
 EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
             'sb_get_mt_state', 'sb_sync', 'sb_visited_size', 'sb_destroy', 'sb_last_error', 'sb_version',
-            'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk')
+            'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk',
+            'sbd_goal_table', 'sbd_expand', 'sbd_pack', 'sbd_owner_claim', 'sbd_apply', 'sbd_emit', 'sbd_hist',
+            'sbd_eq_count', 'sbd_partition', 'sbd_partition_bfs', 'sbd_pack_kept', 'sbd_receive', 'sbd_mark_done')
 
 
 class SplendorBeamError(RuntimeError):

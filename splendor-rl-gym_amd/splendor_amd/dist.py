@@ -1,0 +1,399 @@
+"""Beam sharding across GPUs: one process per GPU, torch.distributed (RCCL over xGMI) for the exchanges.
+
+The global queue of a turn is split into contiguous rank ranges (rank r holds global queue
+positions [off_r, off_r + n_r)), so the (parent rank, ordinal) order that decides first occurrence
+(src/solver.py:446-450) and the noise order (sorted() calls its key in next_queue order,
+src/solver.py:452-456) stay global.  One step, per rank:
+
+  goal      local first rank per pts -> global (+off) -> all_reduce(MIN)  (src/solver.py:438-445)
+  expand    successors of the local parents; a rank-local visited table removes children this rank
+            has generated before (they are already in the global trail) and local same-turn repeats
+  dedup     all_to_all of (key, global tag) to the key's owner (mix64(key) top bits mod world);
+            the owner's shard of the global visited set claims by atomicMin of the tag and answers
+            one byte per record (first occurrence or not); all_to_all back
+  offsets   all_gather of per-rank unique counts -> this rank's next_queue offset k_off
+  emit      survivors' states + scores; noise = accepted MT draw (consumed + k_off + k): every rank
+            runs the same jump-ahead MT19937 stream
+  select    top-W of all scores, stable (score desc, next_queue order asc): MSB radix select with
+            all_reduce(SUM) of 256-bin histograms per pass, for the keep boundary and for the
+            world-1 split boundaries of the kept set; ties at the keep boundary are taken in
+            global order via all_gather of per-rank tie counts
+  rebalance all_to_all of the kept records to their destination range; the receiver stable-sorts
+            by score (records arrive in source order = global next_queue order)
+
+The backend supplies the per-rank compute (HipBackend: libsplendor_beam.so; tests: a Python
+reference backend).  All results are bit-identical to the single-GPU engine and the oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+NONE32 = 0xFFFFFFFF
+BIG = (1 << 62)
+
+
+class Comm:
+    """torch.distributed helpers; gloo works on CPU tensors (device tensors are staged)."""
+
+    def __init__(self, device: torch.device):
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.device = device
+        self.backend = dist.get_backend()
+        self.cpu_coll = self.backend == 'gloo'
+
+    def _to(self, t):
+        return t.cpu() if self.cpu_coll else t
+
+    def _back(self, t):
+        return t.to(self.device) if self.cpu_coll and self.device.type != 'cpu' else t
+
+    def allreduce(self, arr: np.ndarray, op) -> np.ndarray:
+        t = self._to(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device))
+        dist.all_reduce(t, op=op)
+        return t.cpu().numpy()
+
+    def allgather_int(self, v: int) -> np.ndarray:
+        t = self._to(torch.tensor([int(v)], dtype=torch.int64, device=self.device))
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return np.array([int(x.item()) for x in out], dtype=np.int64)
+
+    def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
+        send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
+        recv = torch.zeros_like(send)
+        dist.all_to_all_single(recv, send)
+        return recv.cpu().numpy()
+
+    def alltoall(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
+        s = self._to(send)
+        r = torch.empty(int(sum(recv_counts)), dtype=send.dtype, device=s.device)
+        dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
+        return self._back(r)
+
+    def broadcast_ints(self, vals, src: int) -> list[int]:
+        t = self._to(torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device))
+        dist.broadcast(t, src)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def barrier(self):
+        dist.barrier()
+
+
+def _u64_to_i64(x: int) -> int:
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+class DistSolve:
+    """Sharded speedrun beam solve; every rank calls step() in lockstep."""
+
+    def __init__(self, backend, comm: Comm, *, goal_pts: int, use_heuristic: bool, beam_width: int):
+        self.b = backend
+        self.c = comm
+        self.goal = goal_pts
+        self.heur = use_heuristic
+        self.W = beam_width
+        self.turn = 0
+        self.done = False
+        self.max_pts = 0
+        self.winner = None                      # (turn, global rank)
+        self.counts = [comm.allgather_int(backend.n_local())]   # per turn: per-rank slice sizes
+
+    def offset(self, turn=None) -> int:
+        cnt = self.counts[self.turn if turn is None else turn]
+        return int(cnt[:self.c.rank].sum())
+
+    # ------------------------------------------------------------ goal check (src/solver.py:438-445)
+    def _goal_check(self, st):
+        first = self.b.goal_table().astype(np.int64)
+        off = self.offset()
+        g = np.where(first != NONE32, first + off, BIG)
+        g = self.c.allreduce(g, dist.ReduceOp.MIN)
+        win = -1
+        for p in range(max(self.goal, 0), 256):
+            if g[p] < BIG and (win < 0 or g[p] < win):
+                win = int(g[p])
+        last = -1
+        while True:
+            best, bp = -1, -1
+            for p in range(self.max_pts + 1, 256):
+                if g[p] < BIG and (best < 0 or g[p] < best):
+                    best, bp = int(g[p]), p
+            if best < 0 or (win >= 0 and best > win) or best <= last:
+                break
+            self.max_pts = bp
+            st['records'].append((best, bp))
+            last = best
+        return win
+
+    # ------------------------------------------------------------ one step (src/solver.py:434-457)
+    def step(self) -> dict:
+        c, b = self.c, self.b
+        st = {'turn': self.turn, 'records': [], 'done': False}
+        cnt = self.counts[self.turn]
+        st['n_parents'] = int(cnt.sum())
+        if self.done:
+            st['done'] = True
+            return st
+        win = self._goal_check(st)
+        if win >= 0:
+            self.done, self.winner = True, (self.turn, win)
+            st.update(done=True, winner_rank=win)
+            return st
+        off = self.offset()
+        # local expansion + local filter; candidate records grouped by owner
+        owner_counts, n_raw = b.expand(off, self.turn, c.world)
+        st['n_raw'] = int(c.allreduce(np.array([n_raw]), dist.ReduceOp.SUM)[0])
+        send_key, send_tag = b.pack()
+        recv_counts = c.alltoall_counts(owner_counts)
+        rkey = c.alltoall(send_key, owner_counts, recv_counts)
+        rtag = c.alltoall(send_tag, owner_counts, recv_counts)
+        ret = b.owner_claim(rkey, rtag, self.turn)
+        back = c.alltoall(ret, recv_counts, owner_counts)
+        n_loc = b.apply(back)
+        all_n = c.allgather_int(n_loc)
+        k_off = int(all_n[:c.rank].sum())
+        N = int(all_n.sum())
+        st['n_unique'] = N
+        if N == 0:   # queue empties: `puzzle` is the last parent (src/solver.py:438,459)
+            last = st['n_parents'] - 1
+            self.done, self.winner = True, (self.turn, last)
+            st.update(done=True, winner_rank=last)
+            return st
+        b.emit(k_off, N, off)
+        K = min(N, self.W) if self.heur else N
+        G = c.world
+        if self.heur:
+            pos = []
+            if N > self.W:
+                pos.append(self.W)
+            splits = [max(1, -(-j * K // G)) for j in range(1, G)]
+            pos += splits
+            T, need = self._multiselect(pos)
+            top = None
+            if N > self.W:
+                t0, m0 = T[0], need[0]
+                eq = c.allgather_int(b.eq_count(t0))
+                before = int(eq[:c.rank].sum())
+                quota = max(0, min(m0 - before, int(eq[c.rank])))
+                top = (t0, quota)
+                T = T[1:]
+            dest_counts = b.partition(top, T, G)
+        else:
+            dest_counts = b.partition_bfs(k_off, N, G)
+        lo, hi, par, key = b.pack_kept()
+        recv = c.alltoall_counts(dest_counts)
+        rlo = c.alltoall(lo, dest_counts, recv)
+        rhi = c.alltoall(hi, dest_counts, recv)
+        rpar = c.alltoall(par, dest_counts, recv)
+        rkey = c.alltoall(key, dest_counts, recv)
+        b.receive(rlo, rhi, rpar, rkey, self.heur)
+        self.counts.append(c.allgather_int(b.n_local()))
+        self.turn += 1
+        st['n_kept'] = int(self.counts[-1].sum())
+        return st
+
+    def _multiselect(self, positions):
+        """Global key at each 1-based position of the (score desc) order, 8 MSB passes of 8 bits."""
+        nb = len(positions)
+        pref = np.zeros(nb, dtype=np.uint64)
+        need = np.array(positions, dtype=np.int64)
+        for p in range(8):
+            H = self.c.allreduce(self.b.hist(pref, 8 * p), dist.ReduceOp.SUM).reshape(nb, 256)
+            for j in range(nb):
+                cum = 0
+                d = 255
+                while d > 0 and cum + H[j, d] < need[j]:
+                    cum += int(H[j, d])
+                    d -= 1
+                need[j] -= cum
+                pref[j] = (int(pref[j]) << 8 | d) & 0xFFFFFFFFFFFFFFFF
+        return [int(x) for x in pref], [int(x) for x in need]
+
+    def run(self, max_turns=10_000):
+        trace = []
+        while not self.done and len(trace) < max_turns:
+            trace.append(self.step())
+        return trace
+
+    def path(self):
+        """Root..winner states (src/solver.py:459-464); identical on every rank."""
+        t, r = self.winner
+        out = []
+        while t >= 0:
+            cnt = self.counts[t]
+            offs = np.concatenate([[0], np.cumsum(cnt)])
+            owner = int(np.searchsorted(offs, r, side='right') - 1)
+            vals = [0, 0, 0]
+            if owner == self.c.rank:
+                lo, hi, par = self.b.turn_state(t, r - int(offs[owner]))
+                vals = [_u64_to_i64(lo), _u64_to_i64(hi), par]
+            lo, hi, par = self.c.broadcast_ints(vals, owner)
+            out.append((lo & 0xFFFFFFFFFFFFFFFF, hi & 0xFFFFFFFFFFFFFFFF))
+            r = par
+            t -= 1
+        return out[::-1]
+
+
+class HipBackend:
+    """Per-rank primitives on the MI355X engine (libsplendor_beam.so, sbd_* entry points).
+
+    Exchange buffers are torch tensors on this rank's device, handed to the engine by device
+    pointer; every sbd_* call returns after its device work completed, and the tensors written by
+    collectives are synchronised before the engine reads them.
+    """
+
+    def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
+                 heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0):
+        import ctypes as C
+        from . import _lib as L
+        self.C, self.L = C, L
+        L.ensure_tables()
+        self.lib = L.lib()
+        self._bind()
+        self.device = torch.device('cuda', device_index)
+        torch.cuda.set_device(self.device)
+        cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
+                         device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
+                         flags=0, world_size=int(world), rank=int(rank))
+        h = C.c_void_p()
+        st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
+        L.check(self.lib.sb_create(C.byref(cfg), st, int(root[0]), int(root[1]), C.byref(h)), 'sb_create')
+        self.h = h
+        self.world = world
+
+    def _bind(self):
+        C, lib = self.C, self.lib
+        if getattr(lib, '_sbd_bound', False):
+            return
+        vp, i64, u64, i32 = C.c_void_p, C.c_int64, C.c_uint64, C.c_int32
+        p64 = C.POINTER(C.c_int64)
+        lib.sbd_goal_table.argtypes = [vp, vp]
+        lib.sbd_expand.argtypes = [vp, i64, i32, vp, p64]
+        lib.sbd_pack.argtypes = [vp, vp, vp]
+        lib.sbd_owner_claim.argtypes = [vp, vp, vp, i64, vp]
+        lib.sbd_apply.argtypes = [vp, vp, p64]
+        lib.sbd_emit.argtypes = [vp, u64, u64, i64]
+        lib.sbd_hist.argtypes = [vp, i32, vp, i32, vp]
+        lib.sbd_eq_count.argtypes = [vp, u64, p64]
+        lib.sbd_partition.argtypes = [vp, i32, u64, i64, i32, vp, i32, vp]
+        lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
+        lib.sbd_pack_kept.argtypes = [vp, vp, vp, vp, vp]
+        lib.sbd_receive.argtypes = [vp, vp, vp, vp, vp, i64, i32]
+        lib.sbd_mark_done.argtypes = [vp, i64]
+        lib._sbd_bound = True
+
+    def _chk(self, rc, what):
+        self.L.check(rc, what)
+
+    def _sync(self):
+        torch.cuda.synchronize(self.device)
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.sb_destroy(self.h)
+            self.h = None
+
+    # ---------------------------------------------------------------- queries
+    def n_local(self) -> int:
+        C = self.C
+        nt = C.c_int32()
+        self._chk(self.lib.sb_num_turns(self.h, C.byref(nt)), 'sb_num_turns')
+        n = C.c_int64()
+        self._chk(self.lib.sb_turn_size(self.h, nt.value - 1, C.byref(n)), 'sb_turn_size')
+        return n.value
+
+    def goal_table(self) -> np.ndarray:
+        out = np.zeros(256, np.uint32)
+        self._chk(self.lib.sbd_goal_table(self.h, out.ctypes.data), 'sbd_goal_table')
+        return out
+
+    def turn_state(self, t: int, r: int):
+        lo = np.zeros(1, np.uint64)
+        hi = np.zeros(1, np.uint64)
+        par = np.zeros(1, np.uint32)
+        self._chk(self.lib.sb_read_turn(self.h, t, r, 1, lo.ctypes.data, hi.ctypes.data, par.ctypes.data, None),
+                  'sb_read_turn')
+        return int(lo[0]), int(hi[0]), int(par[0])
+
+    def mt_state(self) -> np.ndarray:
+        out = np.zeros(625, np.uint32)
+        self._chk(self.lib.sb_get_mt_state(self.h, out), 'sb_get_mt_state')
+        return out
+
+    # ---------------------------------------------------------------- step primitives
+    def expand(self, off, turn, world):
+        C = self.C
+        counts = np.zeros(world, np.int64)
+        nraw = C.c_int64()
+        self._chk(self.lib.sbd_expand(self.h, int(off), int(world), counts.ctypes.data, C.byref(nraw)), 'sbd_expand')
+        self.owner_counts = counts
+        return counts, nraw.value
+
+    def _empty(self, n, dtype=torch.int64):
+        return torch.empty(int(n), dtype=dtype, device=self.device)
+
+    def pack(self):
+        n = int(self.owner_counts.sum())
+        key, tag = self._empty(n), self._empty(n)
+        self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), tag.data_ptr()), 'sbd_pack')
+        return key, tag
+
+    def owner_claim(self, rkey, rtag, turn):
+        self._sync()
+        ret = self._empty(rkey.numel(), torch.uint8)
+        self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr(), rtag.data_ptr(), rkey.numel(), ret.data_ptr()),
+                  'sbd_owner_claim')
+        return ret
+
+    def apply(self, back):
+        self._sync()
+        n = self.C.c_int64()
+        self._chk(self.lib.sbd_apply(self.h, back.data_ptr(), self.C.byref(n)), 'sbd_apply')
+        return n.value
+
+    def emit(self, k_off, N, off):
+        self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')
+
+    def hist(self, pref, bits):
+        nb = len(pref)
+        p = np.ascontiguousarray(np.asarray(pref, dtype=np.uint64))
+        out = np.zeros(nb * 256, np.int64)
+        self._chk(self.lib.sbd_hist(self.h, nb, p.ctypes.data, int(bits), out.ctypes.data), 'sbd_hist')
+        return out
+
+    def eq_count(self, T):
+        n = self.C.c_int64()
+        self._chk(self.lib.sbd_eq_count(self.h, int(T), self.C.byref(n)), 'sbd_eq_count')
+        return n.value
+
+    def partition(self, top, splits, G):
+        counts = np.zeros(G, np.int64)
+        sp = np.ascontiguousarray(np.asarray(splits, dtype=np.uint64)) if len(splits) else np.zeros(1, np.uint64)
+        has = top is not None
+        T, q = (top if has else (0, 0))
+        self._chk(self.lib.sbd_partition(self.h, int(has), int(T), int(q), len(splits), sp.ctypes.data, int(G),
+                                         counts.ctypes.data), 'sbd_partition')
+        self.dest_counts = counts
+        return counts
+
+    def partition_bfs(self, k_off, N, G):
+        counts = np.zeros(G, np.int64)
+        self._chk(self.lib.sbd_partition_bfs(self.h, int(k_off), int(N), int(G), counts.ctypes.data),
+                  'sbd_partition_bfs')
+        self.dest_counts = counts
+        return counts
+
+    def pack_kept(self):
+        n = int(self.dest_counts.sum())
+        lo, hi, par, key = self._empty(n), self._empty(n), self._empty(n), self._empty(n)
+        self._chk(self.lib.sbd_pack_kept(self.h, lo.data_ptr(), hi.data_ptr(), par.data_ptr(), key.data_ptr()),
+                  'sbd_pack_kept')
+        return lo, hi, par, key
+
+    def receive(self, lo, hi, par, key, heur):
+        self._sync()
+        self._chk(self.lib.sbd_receive(self.h, lo.data_ptr(), hi.data_ptr(), par.data_ptr(), key.data_ptr(),
+                                       lo.numel(), int(bool(heur))), 'sbd_receive')

@@ -1,0 +1,98 @@
+"""Sharded multi-rank protocol (splendor_amd.dist) on CPU with gloo, world sizes 2 and 3.
+
+Every rank runs DistSolve over the Python reference backend; the concatenated rank slices of every
+turn must equal the single-process oracle's queue (keys, parent links), and the path and final MT
+state must match.  This is the N>1 path of bench.py with the per-rank compute swapped for the
+reference primitives.
+"""
+import json
+import os
+import random
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_c
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
+              os.path.join(os.path.dirname(here), 'oracle'), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from dist_ref_backend import RefBackend
+    from splendor_amd.dist import Comm, DistSolve
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    random.seed(cfg['seed'])
+    st = random.getstate()[1]
+    b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st)
+    solve = DistSolve(b, Comm(torch.device('cpu')), goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
+                      beam_width=cfg['width'])
+    trace = solve.run()
+    out = {'trace': trace, 'counts': [c.tolist() for c in solve.counts], 'path': [list(x) for x in solve.path()],
+           'slices': [[lo, hi, par] for lo, hi, par in b.turns],
+           'mt': b.mt_state().tolist() if cfg['heur'] else None}
+    with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def _run(world, cfg):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
+        return [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
+
+
+CASES = [
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True}),
+    (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True}),
+    (2, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 40, 'seed': 3, 'heur': True}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
+]
+
+
+@pytest.mark.parametrize('world,cfg', CASES)
+def test_sharded_solve_matches_oracle(world, cfg):
+    res = _run(world, cfg)
+    random.seed(cfg['seed'])
+    st = random.getstate()[1]
+    o = oracle_c.OracleSolve(cfg['goal'], use_heuristic=cfg['heur'], heuristic_name=cfg['name'],
+                             beam_width=cfg['width'], mt_state625=st)
+    trace = o.run()
+    assert [t['done'] for t in res[0]['trace']] == [t['done'] for t in trace]
+    for t in range(o.nturns()):
+        lo, hi, par, _ = o.turn_arrays(t)
+        glo = sum((r['slices'][t][0] for r in res), [])
+        ghi = sum((r['slices'][t][1] for r in res), [])
+        gpar = sum((r['slices'][t][2] for r in res), [])
+        assert glo == lo.tolist() and ghi == hi.tolist(), f'turn {t}'
+        if t > 0:
+            assert gpar == par.tolist(), f'turn {t} parents'
+    for a, b in zip(res[0]['trace'], trace):
+        assert a['n_parents'] == b['n_parents'] and a['records'] == [tuple(x) for x in b['records']] or \
+            [list(x) for x in a['records']] == [list(x) for x in b['records']]
+        if not b['done']:
+            assert (a['n_raw'], a['n_unique'], a['n_kept']) == (b['n_raw'], b['n_unique'], b['n_kept'])
+    path = [tuple(p) for p in res[0]['path']]
+    assert path == o.path()
+    assert all([tuple(p) for p in r['path']] == path for r in res)
+    if cfg['heur']:
+        assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    o.close()

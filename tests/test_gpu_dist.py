@@ -1,0 +1,93 @@
+"""Sharded engine on the GPU: world 2/3 ranks on one MI355X (gloo transport, HIP per-rank primitives).
+
+Each rank runs DistSolve over HipBackend (sbd_* entry points of libsplendor_beam.so); the rank slices
+of every turn, concatenated, must equal the oracle's queue (keys and parent links), and the path and
+MT state must match.  (RCCL needs one GPU per rank; the 8-GPU RCCL run is bench.py --gpus N.)
+"""
+import json
+import os
+import random
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_c
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
+              os.path.join(os.path.dirname(here), 'oracle'), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from splendor_amd.dist import Comm, DistSolve, HipBackend
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    random.seed(cfg['seed'])
+    st = random.getstate()[1]
+    b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
+                   heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st)
+    solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
+    trace = solve.run()
+    slices = []
+    for t in range(len(solve.counts)):
+        n = int(solve.counts[t][rank])
+        rows = [b.turn_state(t, r) for r in range(n)]
+        slices.append([[x[0] for x in rows], [x[1] for x in rows], [x[2] for x in rows]])
+    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'slices': slices,
+           'mt': b.mt_state().tolist()}
+    with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
+        json.dump(out, f)
+    b.close()
+    dist.destroy_process_group()
+
+
+CASES = [
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True}),
+    (3, {'goal': 6, 'hid': 0, 'name': 'simple', 'width': 250, 'seed': 2, 'heur': True}),
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
+]
+
+
+@pytest.mark.parametrize('world,cfg', CASES)
+def test_sharded_engine_matches_oracle(world, cfg):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
+        res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
+    random.seed(cfg['seed'])
+    st = random.getstate()[1]
+    o = oracle_c.OracleSolve(cfg['goal'], use_heuristic=cfg['heur'], heuristic_name=cfg['name'],
+                             beam_width=cfg['width'], mt_state625=st)
+    trace = o.run()
+    assert len(res[0]['trace']) == len(trace)
+    for t in range(o.nturns()):
+        lo, hi, par, _ = o.turn_arrays(t)
+        assert sum((r['slices'][t][0] for r in res), []) == lo.tolist(), f'turn {t}'
+        assert sum((r['slices'][t][1] for r in res), []) == hi.tolist(), f'turn {t}'
+        if t > 0:
+            assert sum((r['slices'][t][2] for r in res), []) == par.tolist(), f'turn {t} parents'
+    for a, b in zip(res[0]['trace'], trace):
+        if not b['done']:
+            assert (a['n_raw'], a['n_unique'], a['n_kept']) == (b['n_raw'], b['n_unique'], b['n_kept'])
+    assert [tuple(p) for p in res[0]['path']] == o.path()
+    if cfg['heur']:
+        assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    o.close()
