@@ -1,0 +1,77 @@
+"""bench.py --gpus N (N > 1): the sharded beam step, one process per GPU, RCCL over xGMI.
+
+Launched by `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...`.  Weak scaling:
+every GPU holds --width states (global beam_width = N x width; N=8 x 4M = 32M is config C5's width).
+The seeded solve runs from the root until the global beam is full (setup), then --warmup untimed
+steps, then exactly --steps timed steps, each bracketed by barrier + device synchronize; the time is
+the max over ranks and value = all parents expanded / that time.
+"""
+import json
+import os
+import random
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def main(args):
+    from bench import HBM_PEAK_GBS, METRIC, step_bytes
+    from splendor_amd.dist import Comm, DistSolve, HipBackend
+    from splendor_amd.engine import HEURISTIC_IDS
+    backend = os.environ.get('SB_DIST_BACKEND', 'nccl')
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = torch.cuda.device_count()
+    dev = local if backend == 'nccl' else local % max(ndev, 1)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend, device_id=torch.device('cuda', dev) if backend == 'nccl' else None)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    W = args.width * world
+    random.seed(args.seed)
+    st = random.getstate()[1]
+    b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=255, use_heuristic=True,
+                   heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=st)
+    comm = Comm(b.device)
+    solve = DistSolve(b, comm, goal_pts=255, use_heuristic=True, beam_width=W)
+    setup = 0
+    while True:
+        s = solve.step()
+        setup += 1
+        if s.get('n_kept', 0) >= W or s['done']:
+            break
+    for _ in range(args.warmup):
+        solve.step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    per = [solve.step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    el_max = float(comm.allreduce(np.array([int(el * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9
+    parents = sum(p['n_parents'] for p in per)
+    raw = sum(p['n_raw'] for p in per)
+    uniq = sum(p['n_unique'] for p in per)
+    kept = sum(p['n_kept'] for p in per)
+    if rank == 0:
+        gbs = step_bytes(parents, raw, uniq, kept) / el_max / 1e9
+        out = {
+            'metric': METRIC, 'value': round(parents / el_max, 1), 'unit': 'states/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el_max / args.steps * 1e3, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64+f64',
+            'data': f'synthetic: seeded solve trajectory (random.seed({args.seed})), saturated turns '
+                    f'{setup + args.warmup}..{setup + args.warmup + args.steps - 1}',
+            'config': {'workload': f'speedrun goal_pts=15 -u -H {args.heuristic} beam_width={W} '
+                                   f'({args.width} per GPU; C5 at 8 GPUs x 4M)',
+                       'beam_width': W, 'heuristic': args.heuristic, 'seed': args.seed,
+                       'parallelism': f'beam sharded over {world} GPUs ({backend})',
+                       'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3)},
+            'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
+                         'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
+            'cpu_baseline': None,
+        }
+        print(json.dumps(out), flush=True)
+    b.close()
+    dist.destroy_process_group()

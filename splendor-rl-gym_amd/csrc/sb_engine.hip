@@ -782,7 +782,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         int lg = cfg->visited_log2;
         if (lg <= 0) {
             // ~10 unique children per parent per turn, ~20 turns, <= 50% load
-            double want = (double)cfg->beam_width * 10.0 * 20.0 * 2.0;
+            double want = (double)cfg->beam_width * 10.0 * 20.0 * 2.0 / (cfg->world_size > 1 ? cfg->world_size : 1);
             lg = 20;
             while ((double)(1ull << lg) < want && lg < 31) lg++;
         }
@@ -821,7 +821,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         hipLaunchKernelGGL(k_pts_first, dim3(1), dim3(256), 0, E.s, t0.hi, t0.n, E.d_small + 8);
         // MT chunk = 256 producers x twists x 624 words ~ 16 draws per beam slot; ring >= 4 chunks
         int64_t twists = 1;
-        while (twists < 512 && (double)twists * 256 * 624 < (double)cfg->beam_width * 16) twists <<= 1;
+        while (twists < 4096 && (double)twists * 256 * 624 < (double)cfg->beam_width * 16) twists <<= 1;
         uint64_t ring = 1ull << 24;
         while ((ring < (uint64_t)cfg->beam_width * 64 || ring < 4ull * 256 * 624 * (uint64_t)twists) &&
                ring < (1ull << 35))

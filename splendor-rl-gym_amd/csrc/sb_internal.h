@@ -82,11 +82,13 @@ struct MTProducers {
     uint32_t* chunk_poly = nullptr;
     void init(const uint32_t origin[624], int P, int64_t twists, hipStream_t st);
     void gen_chunk(uint32_t* out, hipStream_t st);   // P*L tempered words
+    void gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st);   // accepted values per producer
     void release();
 };
 struct NoiseStream {
     MTProducers prod;
-    DBuf<uint32_t> raw;            // raw tempered words staging (one chunk)
+    DBuf<uint32_t> raw;            // raw tempered words (host-emitted lead block)
+    DBuf<uint8_t> stage;           // per-producer accepted values of one chunk
     DBuf<uint8_t> ring;            // accepted randint values 1..100
     uint64_t ring_mask = 0;
     uint64_t produced = 0;         // accepted values written so far (host mirror, valid after sync)

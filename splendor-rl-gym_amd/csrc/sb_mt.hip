@@ -10,8 +10,9 @@
 //   k_mt_jump     advances producer windows by J words: w(n+J)[j] = XOR_{g_i=1} y_{n+1+i+j} with
 //                 g = x^(J-1) mod phi (sb_gf2.hip); the sequence y is extended in LDS, the
 //                 correlation runs one wave per (64 outputs x poly slice), uniform over poly bits;
-//   k_mt_count/k_mt_write   order-preserving compaction of accepted draws into a ring of u8
-//                 values, so next_queue element k reads ring[(consumed + k) & mask].
+//   compaction  each producer writes only its accepted draws (in order) to a staging segment
+//               (ballot + wave-count scan per twist); k_mt_place copies the segments into a ring of u8
+//               values, so next_queue element k reads ring[(consumed + k) & mask].
 #include <string.h>
 
 #include "sb_block.h"
@@ -87,15 +88,22 @@ __global__ __launch_bounds__(MT_NT) void k_mt_write(const uint32_t* __restrict__
     }
 }
 
-// P producers, one workgroup each; producer b runs `twists` twists from window b.
+// P producers, one workgroup each; producer b runs `twists` twists from window b.  Raw mode writes
+// the tempered words (debug); compact mode writes only the accepted randint values (1..100) of the
+// segment, in order, to stage[b * L ..] and their count to counts[b] (fused accept compaction).
+template <bool RAW>
 __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
+                                                     uint8_t* __restrict__ stage, uint32_t* __restrict__ counts,
                                                      int64_t twists) {
     __shared__ uint32_t buf[2][624];
-    const int t = threadIdx.x;
+    __shared__ uint32_t wc[10];
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const int64_t b = blockIdx.x;
     if (t < 624) buf[0][t] = wins[b * 624 + t];
     __syncthreads();
-    uint32_t* o = out + b * twists * 624;
+    uint32_t* o = RAW ? out + b * twists * 624 : nullptr;
+    uint8_t* sg = RAW ? nullptr : stage + b * twists * 624;
+    uint32_t run = 0;
     int cur = 0;
     for (int64_t w = 0; w < twists; w++) {
         uint32_t* A = buf[cur];
@@ -107,9 +115,38 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
         if (t < 169) B[454 + t] = mt_mix(A[454 + t], A[455 + t], B[227 + t]);
         else if (t == 169) B[623] = mt_mix(A[623], B[0], B[396]);
         __syncthreads();
-        if (t < 624) o[w * 624 + t] = mt_temper(B[t]);
+        const uint32_t y = t < 624 ? mt_temper(B[t]) : 0u;
+        if (RAW) {
+            if (t < 624) o[w * 624 + t] = y;
+        } else {
+            const bool acc = t < 624 && (y >> 25) < 100u;
+            const uint64_t m = __ballot(acc);
+            if (lane == 0) wc[wv] = __popcll(m);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+#pragma unroll
+            for (int x = 0; x < 10; x++) {
+                const uint32_t c = wc[x];
+                before += x < wv ? c : 0u;
+                total += c;
+            }
+            if (acc) sg[run + before + __popcll(m & lanemask_lt())] = (uint8_t)((y >> 25) + 1);
+            run += total;
+        }
         cur ^= 1;
     }
+    if (!RAW && t == 0) counts[b] = run;
+}
+
+// copy each producer's accepted values to the ring at produced + exclusive offset
+__global__ __launch_bounds__(256) void k_mt_place(const uint8_t* __restrict__ stage, int64_t seg,
+                                                  const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offs,
+                                                  uint8_t* __restrict__ ring, uint64_t ring_mask, uint64_t produced) {
+    const int64_t b = blockIdx.x;
+    const uint32_t n = counts[b];
+    const uint64_t base = produced + offs[b];
+    const uint8_t* src = stage + b * seg;
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) ring[(base + j) & ring_mask] = src[j];
 }
 
 constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
@@ -182,7 +219,17 @@ void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipS
 void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
     if (chunk > 0)   // every producer jumps P*L ahead of its previous segment start
         hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
-    hipLaunchKernelGGL(k_mt_gen_par, dim3(P), dim3(640), 0, st, d_win, out, twists);
+    hipLaunchKernelGGL(k_mt_gen_par<true>, dim3(P), dim3(640), 0, st, d_win, out, (uint8_t*)nullptr,
+                       (uint32_t*)nullptr, twists);
+    SB_HIP(hipGetLastError());
+    chunk++;
+}
+
+void MTProducers::gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st) {
+    if (chunk > 0)
+        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
+    hipLaunchKernelGGL(k_mt_gen_par<false>, dim3(P), dim3(640), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
+                       twists);
     SB_HIP(hipGetLastError());
     chunk++;
 }
@@ -238,10 +285,19 @@ void noise_generate_async(NoiseStream& ns, hipStream_t st) {
     const uint64_t n = noise_chunk_words(ns);
     const uint64_t room = ns.ring_mask + 1 - (ns.produced - ns.consumed);
     if (n > room) return;   // accepted draws <= words: never overrun unconsumed values
-    ns.raw.ensure((size_t)n);
-    ns.prod.gen_chunk(ns.raw.p, st);
-    compact_accepted(ns, ns.raw.p, (int64_t)n, st);
+    const int P = ns.prod.P;
+    ns.stage.ensure((size_t)n);
+    ns.scan.tiles.ensure((size_t)2 * P);
+    uint32_t* counts = ns.scan.tiles.p;
+    uint32_t* offs = ns.scan.tiles.p + P;
+    ns.prod.gen_chunk_accepted(ns.stage.p, counts, st);
+    SB_HIP(hipMemcpyAsync(offs, counts, (size_t)P * 4, hipMemcpyDeviceToDevice, st));
+    scan_tiles_inplace(offs, P, ns.d_total, st);
+    hipLaunchKernelGGL(k_mt_place, dim3(P), dim3(256), 0, st, ns.stage.p, (int64_t)ns.prod.twists * 624, counts, offs,
+                       ns.ring.p, ns.ring_mask, ns.produced);
+    SB_HIP(hipMemcpyAsync(ns.h_total, ns.d_total, 4, hipMemcpyDeviceToHost, st));
     SB_HIP(hipEventRecord(ns.ev_ready, st));
+    SB_HIP(hipGetLastError());
     ns.pending = true;
 }
 
@@ -280,6 +336,7 @@ void noise_free(NoiseStream& ns) {
     if (ns.ev_ready) (void)hipEventDestroy(ns.ev_ready);
     ns.prod.release();
     ns.raw.release();
+    ns.stage.release();
     ns.ring.release();
     ns.scan.tiles.release();
     ns.d_total = nullptr;
