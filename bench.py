@@ -48,6 +48,21 @@ def expand_bytes(n_parents, n_raw, n_cand_new):
     return 16 * n_parents + 21 * n_raw + 16 * n_cand_new + 24 * n_parents
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary (profiles/)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_profile_summary.json')))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            v = d['pmc'][kernel]['hbm_bytes_per_launch']
+            t = d['timed'][kernel]['avg_ns']
+            return v, t, os.path.relpath(f, REPO)
+        except (KeyError, ValueError, OSError):
+            continue
+    return None, None, None
+
+
 def step_bytes(n_parents, n_raw, n_unique, n_kept):
     """SURVEY.md §8(d) whole-step model: 28 + 20 b_raw + 37 b_uniq + 33 per parent (with our 16 B state)."""
     return 28 * n_parents + 20 * n_raw + 37 * n_unique + 33 * n_kept
@@ -152,10 +167,16 @@ def main():
         'phases_ms': phases,
         'roofline': {'bound': 'hbm', 'kernel': dom.replace('ms_', 'k_'), 'achieved': round(achieved, 2),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
-                     'traffic': None},
+                     'algorithmic_bytes_per_launch': int(byt), 'launch_ms': ms_dom, 'traffic': None},
         'step_model_GBps': round(step_bytes(parents, raw, uniq, kept) / elapsed / 1e9, 2),
         'cpu_baseline': None,
     }
+    tr, tns, src = pmc_traffic(dom.replace('ms_', 'k_'))
+    if tr is not None:
+        out['roofline']['traffic'] = int(tr)
+        out['roofline']['traffic_GBps'] = round(tr / (tns * 1e-9) / 1e9, 1)
+        out['roofline']['traffic_source'] = f'{src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; ' \
+                                            f'hbm = (2*FETCH + WRITE) KiB, gfx950 correction)'
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, args.cpu_budget_s)
     print(json.dumps(out))
