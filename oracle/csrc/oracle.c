@@ -506,3 +506,367 @@ int oc_get_mt_state(oc_handle* h, uint32_t* out625) {
     return 0;
 }
 uint64_t oc_visited_size(oc_handle* h) { return h->visited.n; }
+
+/* ====================================================================================== */
+/* Realistic multi-player mode (src/solver.py:25-200, 471-860): TEST INFRASTRUCTURE ONLY.
+ *
+ *   MultiPlayerState.__hash__ = hash((players, pool, visible, current_player))   (:495-500)
+ *     with PlayerState hashed as its field tuple (player_id, cards, bonus, gems, pts, saved)
+ *   __iter__: buys over visible cards t1+t2+t3 (:574-632, can_afford :192-200, market.buy_card
+ *     :121-170 appends the deck head to the END of the tier, pool.return_gems :75-80, final-round
+ *     bookkeeping :606-615), then realistic takes (:664-748): combinations of available colours
+ *     taken 3 (hand + 3 <= 10), then 2-same by colour (pool >= 4, hand + 2 <= 10)
+ *   solve (:750-860): is_game_over before the max_pts record, always sorts with
+ *     multi_competitive_heuristic (:778-812), 1000-turn cap (:849-852)
+ *
+ * Packed form (12 x u64, shared with the engine and the host):
+ *   w[2i], w[2i+1]  player i (i < 4): cards lo | hi = cards 64..89, gems 26+3c, pts 41..48, saved 49..63
+ *   w[8]  pool 3 bits x5 (0..14) | cp 15..16 | frt 17 | frp 18..20 (7 = None) | deck pointers 6 bits
+ *         x3 (21..38) | visible counts 3 bits x3 (39..47)
+ *   w[9]  tier-1 visible 4 x 7 bits (0..27), tier-2 visible (28..55);  w[10] tier-3 visible (0..27)
+ */
+#define RW 12
+typedef struct { int P, target; int tier[3][40]; int tlen[3]; } rgame_t;
+typedef struct { uint64_t w[RW]; } rst_t;
+
+static inline int r_pool(const rst_t* s, int c) { return (int)((s->w[8] >> (3 * c)) & 7); }
+static inline int r_cp(const rst_t* s) { return (int)((s->w[8] >> 15) & 3); }
+static inline int r_frt(const rst_t* s) { return (int)((s->w[8] >> 17) & 1); }
+static inline int r_frp(const rst_t* s) { int v = (int)((s->w[8] >> 18) & 7); return v == 7 ? -1 : v; }
+static inline int r_dptr(const rst_t* s, int t) { return (int)((s->w[8] >> (21 + 6 * t)) & 63); }
+static inline int r_nvis(const rst_t* s, int t) { return (int)((s->w[8] >> (39 + 3 * t)) & 7); }
+static inline int r_vis(const rst_t* s, int t, int j) {
+    uint64_t w = t < 2 ? s->w[9] >> (28 * t) : s->w[10];
+    return (int)((w >> (7 * j)) & 127);
+}
+static inline st_t r_player(const rst_t* s, int i) { st_t p = {s->w[2 * i], s->w[2 * i + 1]}; return p; }
+static inline void r_set_player(rst_t* s, int i, st_t p) { s->w[2 * i] = p.lo; s->w[2 * i + 1] = p.hi; }
+
+static void r_set_meta(rst_t* s, const int pool[5], int cp, int frt, int frp, const int dptr[3], const int nvis[3],
+                       const int vis[3][4]) {
+    uint64_t m = 0;
+    for (int c = 0; c < 5; c++) m |= (uint64_t)pool[c] << (3 * c);
+    m |= (uint64_t)cp << 15;
+    m |= (uint64_t)(frt ? 1 : 0) << 17;
+    m |= (uint64_t)(frp < 0 ? 7 : frp) << 18;
+    for (int t = 0; t < 3; t++) m |= (uint64_t)dptr[t] << (21 + 6 * t);
+    for (int t = 0; t < 3; t++) m |= (uint64_t)nvis[t] << (39 + 3 * t);
+    s->w[8] = m;
+    uint64_t v0 = 0, v1 = 0;
+    for (int t = 0; t < 3; t++)
+        for (int j = 0; j < nvis[t]; j++) {
+            uint64_t c = (uint64_t)vis[t][j];
+            if (t == 0) v0 |= c << (7 * j);
+            else if (t == 1) v0 |= c << (28 + 7 * j);
+            else v1 |= c << (7 * j);
+        }
+    s->w[9] = v0;
+    s->w[10] = v1;
+}
+
+static uint64_t th_tuple(const uint64_t* lanes, int n) {
+    uint64_t acc = XXP5;
+    for (int i = 0; i < n; i++) acc = th_step(acc, lanes[i]);
+    return th_fin(acc, (uint64_t)n);
+}
+
+static uint64_t r_key(const rgame_t* G, const rst_t* s) {
+    uint64_t hp[4];
+    for (int i = 0; i < G->P; i++) {
+        st_t p = r_player(s, i);
+        int b[NCOL], g[NCOL];
+        st_bonus(p, b);
+        uint64_t lb[5], lg[5];
+        for (int c = 0; c < 5; c++) { lb[c] = (uint64_t)b[c]; g[c] = st_gem(p, c); lg[c] = (uint64_t)g[c]; }
+        uint64_t f[6] = {(uint64_t)i, hash_cards(p), th_tuple(lb, 5), th_tuple(lg, 5), (uint64_t)st_pts(p),
+                         (uint64_t)st_saved(p)};
+        hp[i] = th_tuple(f, 6);
+    }
+    uint64_t lp[5], lv[12];
+    for (int c = 0; c < 5; c++) lp[c] = (uint64_t)r_pool(s, c);
+    int nv = 0;
+    for (int t = 0; t < 3; t++)
+        for (int j = 0; j < r_nvis(s, t); j++) lv[nv++] = (uint64_t)r_vis(s, t, j);
+    uint64_t outer[4] = {th_tuple(hp, G->P), th_tuple(lp, 5), th_tuple(lv, nv), (uint64_t)r_cp(s)};
+    return th_tuple(outer, 4);
+}
+
+static int r_can_afford(st_t p, int c) {
+    int b[NCOL];
+    st_bonus(p, b);
+    for (int i = 0; i < NCOL; i++)
+        if (st_gem(p, i) + b[i] < DECK[c].cost[i]) return 0;
+    return 1;
+}
+
+static void r_unpack_meta(const rst_t* s, int pool[5], int dptr[3], int nvis[3], int vis[3][4]) {
+    for (int c = 0; c < 5; c++) pool[c] = r_pool(s, c);
+    for (int t = 0; t < 3; t++) {
+        dptr[t] = r_dptr(s, t);
+        nvis[t] = r_nvis(s, t);
+        for (int j = 0; j < nvis[t]; j++) vis[t][j] = r_vis(s, t, j);
+    }
+}
+
+static int r_successors(const rgame_t* G, const rst_t* s, rst_t* out) {
+    const int cur = r_cp(s), nxt = (cur + 1) % G->P, frt = r_frt(s), frp = r_frp(s);
+    int pool[5], dptr[3], nvis[3], vis[3][4];
+    r_unpack_meta(s, pool, dptr, nvis, vis);
+    st_t me = r_player(s, cur);
+    int g[NCOL], b[NCOL];
+    for (int c = 0; c < NCOL; c++) g[c] = st_gem(me, c);
+    st_bonus(me, b);
+    int n = 0;
+    for (int t = 0; t < 3; t++)
+        for (int j = 0; j < nvis[t]; j++) {       /* buys, visible order t1+t2+t3 */
+            const int card = vis[t][j];
+            if (st_has(me, card) || !r_can_afford(me, card)) continue;
+            int ng[NCOL], sv = 0, np[5];
+            for (int c = 0; c < NCOL; c++) {
+                int cc = DECK[card].cost[c] - b[c]; if (cc < 0) cc = 0;
+                if (cc < DECK[card].cost[c]) sv += DECK[card].cost[c] - cc;
+                int x = g[c] - cc; ng[c] = x < 0 ? 0 : x;
+                np[c] = pool[c] + (g[c] - ng[c]);
+            }
+            uint64_t lo = me.lo, hi = me.hi;
+            if (card < 64) lo |= 1ull << card; else hi |= 1ull << (card - 64);
+            const int npts = st_pts(me) + DECK[card].pt;
+            st_t pl = st_make(lo, hi, ng, npts, st_saved(me) + sv);
+            int nv2[3] = {nvis[0], nvis[1], nvis[2]}, vis2[3][4], dp2[3] = {dptr[0], dptr[1], dptr[2]};
+            memcpy(vis2, vis, sizeof vis2);
+            for (int k = j; k + 1 < nv2[t]; k++) vis2[t][k] = vis2[t][k + 1];
+            nv2[t]--;
+            if (dp2[t] < G->tlen[t] - 4) { vis2[t][nv2[t]++] = G->tier[t][4 + dp2[t]]; dp2[t]++; }
+            const int frt2 = frt || npts >= G->target;
+            const int frp2 = frt ? frp : (frt2 ? cur : -1);
+            rst_t c2 = *s;
+            r_set_player(&c2, cur, pl);
+            r_set_meta(&c2, np, nxt, frt2, frp2, dp2, nv2, vis2);
+            out[n++] = c2;
+        }
+    int avail[5], na = 0, tot = 0;
+    for (int c = 0; c < 5; c++) { if (pool[c] > 0) avail[na++] = c; tot += g[c]; }
+    for (int x = 0; x < na; x++)                  /* combinations(available, 3) */
+        for (int y = x + 1; y < na; y++)
+            for (int z = y + 1; z < na; z++) {
+                if (tot + 3 > 10) continue;
+                int ng[NCOL], np[5];
+                for (int c = 0; c < 5; c++) { ng[c] = g[c]; np[c] = pool[c]; }
+                int cs[3] = {avail[x], avail[y], avail[z]};
+                for (int k = 0; k < 3; k++) { ng[cs[k]]++; np[cs[k]]--; }
+                rst_t c2 = *s;
+                r_set_player(&c2, cur, st_make(me.lo, me.hi, ng, st_pts(me), st_saved(me)));
+                r_set_meta(&c2, np, nxt, frt, frp, dptr, nvis, vis);
+                out[n++] = c2;
+            }
+    for (int x = 0; x < na; x++) {                /* two of one colour */
+        const int c0 = avail[x];
+        if (pool[c0] < 4 || tot + 2 > 10) continue;
+        int ng[NCOL], np[5];
+        for (int c = 0; c < 5; c++) { ng[c] = g[c]; np[c] = pool[c]; }
+        ng[c0] += 2; np[c0] -= 2;
+        rst_t c2 = *s;
+        r_set_player(&c2, cur, st_make(me.lo, me.hi, ng, st_pts(me), st_saved(me)));
+        r_set_meta(&c2, np, nxt, frt, frp, dptr, nvis, vis);
+        out[n++] = c2;
+    }
+    return n;
+}
+
+/* multi_competitive_heuristic (src/solver.py:778-812) */
+static double r_score(const rgame_t* G, const rst_t* s, double noise) {
+    const int cp = r_cp(s), prev = ((cp - 1) % G->P + G->P) % G->P;
+    st_t me = r_player(s, prev), op = r_player(s, cp);
+    int bm[NCOL], bo[NCOL];
+    st_bonus(me, bm);
+    st_bonus(op, bo);
+    const int mp = st_pts(me), opp = st_pts(op);
+    double pd = mp > opp ? pow((double)(mp - opp), 2.5) : -pow((double)(opp - mp), 2.5);
+    int mr = 0, orr = 0, div = 0;
+    for (int c = 0; c < NCOL; c++) { mr += st_gem(me, c) + bm[c] * 2; orr += st_gem(op, c) + bo[c] * 2; div += bm[c] > 0; }
+    double rd = mr > orr ? pow((double)(mr - orr), 0.5) : 0.0;
+    int ma = 0, oa = 0;
+    for (int t = 0; t < 3; t++)
+        for (int j = 0; j < r_nvis(s, t); j++) { int c = r_vis(s, t, j); ma += r_can_afford(me, c); oa += r_can_afford(op, c); }
+    const int mc = (ma - oa) * 5;
+    double r = pd * 100;
+    r = r + rd * 20;
+    r = r + (double)mc;
+    r = r + pow((double)div, 0.5) * 3;
+    return r + noise;
+}
+
+static int r_game_over(const rgame_t* G, const rst_t* s) {
+    if (!r_frt(s)) {
+        for (int i = 0; i < G->P; i++) if (st_pts(r_player(s, i)) >= G->target) return 1;
+        return 0;
+    }
+    return r_cp(s) == r_frp(s);
+}
+
+/* total order of doubles as u64 (negatives flipped, -0.0 == +0.0 as in Python) */
+static inline uint64_t f64_key(double d) {
+    if (d == 0.0) d = 0.0;
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+/* ---- ctypes surface for tests */
+static int r_load_game(rgame_t* G, const int32_t* params, const int32_t* tiers) {
+    G->P = params[0]; G->target = params[1];
+    for (int t = 0; t < 3; t++) { G->tlen[t] = params[2 + t]; for (int k = 0; k < G->tlen[t]; k++) G->tier[t][k] = tiers[t * 40 + k]; }
+    return (G->P >= 2 && G->P <= 4) ? 0 : -1;
+}
+
+uint64_t ort_key(const int32_t* params, const int32_t* tiers, const uint64_t* w) {
+    rgame_t G; r_load_game(&G, params, tiers);
+    rst_t s; memcpy(s.w, w, sizeof s.w);
+    return r_key(&G, &s);
+}
+
+int ort_successors(const int32_t* params, const int32_t* tiers, const uint64_t* w, uint64_t* out, uint64_t* keys) {
+    rgame_t G; r_load_game(&G, params, tiers);
+    rst_t s; memcpy(s.w, w, sizeof s.w);
+    rst_t kids[64];
+    int n = r_successors(&G, &s, kids);
+    for (int k = 0; k < n; k++) { memcpy(out + k * RW, kids[k].w, sizeof kids[k].w); keys[k] = r_key(&G, &kids[k]); }
+    return n;
+}
+
+double ort_score(const int32_t* params, const int32_t* tiers, const uint64_t* w, int k) {
+    rgame_t G; r_load_game(&G, params, tiers);
+    rst_t s; memcpy(s.w, w, sizeof s.w);
+    return r_score(&G, &s, (double)k * 0.01);
+}
+
+int ort_game_over(const int32_t* params, const int32_t* tiers, const uint64_t* w) {
+    rgame_t G; r_load_game(&G, params, tiers);
+    rst_t s; memcpy(s.w, w, sizeof s.w);
+    return r_game_over(&G, &s);
+}
+
+/* ---- realistic beam solve (src/solver.py:774-860) */
+typedef struct { rst_t* st; uint32_t* par; int64_t n; } rturn_t;
+typedef struct {
+    rgame_t G;
+    int64_t beam_width;
+    int turn, done, max_pts;
+    int64_t winner_rank;
+    mt_t mt;
+    hset_t visited;
+    rturn_t* turns; int nturns, capturns;
+} ort_handle;
+
+static void r_push(ort_handle* h, rst_t* st, uint32_t* par, int64_t n) {
+    if (h->nturns == h->capturns) {
+        h->capturns = h->capturns ? h->capturns * 2 : 64;
+        h->turns = (rturn_t*)realloc(h->turns, sizeof(rturn_t) * h->capturns);
+    }
+    h->turns[h->nturns].st = st; h->turns[h->nturns].par = par; h->turns[h->nturns].n = n;
+    h->nturns++;
+}
+
+ort_handle* ort_create(const int32_t* params, const int32_t* tiers, int64_t beam_width, const uint32_t* mt_state625,
+                       const uint64_t* root_w) {
+    if (!DECK_READY) return NULL;
+    ort_handle* h = (ort_handle*)calloc(1, sizeof(ort_handle));
+    if (r_load_game(&h->G, params, tiers)) { free(h); return NULL; }
+    h->beam_width = beam_width;
+    memcpy(h->mt.mt, mt_state625, 624 * 4); h->mt.idx = (int)mt_state625[624];
+    hs_init(&h->visited, 1u << 16);
+    rst_t* root = (rst_t*)malloc(sizeof(rst_t)); memcpy(root->w, root_w, sizeof root->w);
+    uint32_t* rp = (uint32_t*)malloc(4); rp[0] = 0xFFFFFFFFu;
+    r_push(h, root, rp, 1);
+    hs_insert(&h->visited, r_key(&h->G, root));
+    h->winner_rank = -1;
+    return h;
+}
+
+void ort_destroy(ort_handle* h) {
+    if (!h) return;
+    for (int t = 0; t < h->nturns; t++) { free(h->turns[t].st); free(h->turns[t].par); }
+    free(h->turns); free(h->visited.slot); free(h);
+}
+
+int ort_step(ort_handle* h, oc_stats* out) {
+    memset(out, 0, sizeof *out);
+    if (h->done) { out->done = 1; out->winner_rank = h->winner_rank; return 0; }
+    rturn_t* cur = &h->turns[h->nturns - 1];
+    out->n_parents = cur->n;
+    for (int64_t r = 0; r < cur->n; r++) {       /* game over first, then the record (:826-836) */
+        if (r_game_over(&h->G, &cur->st[r])) {
+            h->done = 1; h->winner_rank = r; out->done = 1; out->winner_rank = r; out->mt_words = h->mt.words;
+            return 0;
+        }
+        int mp = 0;
+        for (int i = 0; i < h->G.P; i++) { int p = st_pts(r_player(&cur->st[r], i)); if (p > mp) mp = p; }
+        if (mp > h->max_pts) {
+            h->max_pts = mp;
+            if (out->n_records < 32) { out->record_rank[out->n_records] = r; out->record_pts[out->n_records] = mp; out->n_records++; }
+        }
+    }
+    int64_t cap = cur->n * 32 + 64, nq = 0, nraw = 0;
+    rst_t* nxt = (rst_t*)malloc(sizeof(rst_t) * cap);
+    uint32_t* npar = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    rst_t kids[64];
+    for (int64_t r = 0; r < cur->n; r++) {
+        int nk = r_successors(&h->G, &cur->st[r], kids);
+        nraw += nk;
+        for (int k = 0; k < nk; k++) {
+            if (!hs_insert(&h->visited, r_key(&h->G, &kids[k]))) continue;
+            if (nq == cap) { cap *= 2; nxt = (rst_t*)realloc(nxt, sizeof(rst_t) * cap); npar = (uint32_t*)realloc(npar, 4 * cap); }
+            nxt[nq] = kids[k]; npar[nq] = (uint32_t)r; nq++;
+        }
+    }
+    out->n_raw = nraw; out->n_unique = nq;
+    if (nq == 0) {
+        h->done = 1; h->winner_rank = cur->n - 1; out->done = 1; out->winner_rank = cur->n - 1;
+        free(nxt); free(npar); out->mt_words = h->mt.words;
+        return 0;
+    }
+    uint64_t* key = (uint64_t*)malloc(8 * nq);
+    uint32_t* idx = (uint32_t*)malloc(4 * nq);
+    for (int64_t i = 0; i < nq; i++) key[i] = f64_key(r_score(&h->G, &nxt[i], (double)mt_randint100(&h->mt) * 0.01));
+    sort_desc_stable(key, idx, nq);
+    int64_t nk = nq < h->beam_width ? nq : h->beam_width;
+    rst_t* ks = (rst_t*)malloc(sizeof(rst_t) * nk);
+    uint32_t* kp = (uint32_t*)malloc(4 * nk);
+    for (int64_t i = 0; i < nk; i++) { ks[i] = nxt[idx[i]]; kp[i] = npar[idx[i]]; }
+    free(key); free(idx); free(nxt); free(npar);
+    r_push(h, ks, kp, nk);
+    out->n_kept = nk;
+    h->turn++;
+    if (h->turn > 1000) {   /* safety cap (:849-852): `puzzle` is the last parent of this turn */
+        h->done = 1; h->winner_rank = cur->n - 1; out->done = 1; out->winner_rank = cur->n - 1;
+        /* the reference stops with the previous queue's last state; drop the new turn from the path */
+        h->nturns--; free(ks); free(kp);
+    }
+    out->mt_words = h->mt.words;
+    return 0;
+}
+
+int64_t ort_turn_size(ort_handle* h, int t) { return (t < 0 || t >= h->nturns) ? -1 : h->turns[t].n; }
+int ort_nturns(ort_handle* h) { return h->nturns; }
+int ort_read_turn(ort_handle* h, int t, uint64_t* w, uint32_t* par, uint64_t* key) {
+    if (t < 0 || t >= h->nturns) return -1;
+    rturn_t* tt = &h->turns[t];
+    for (int64_t i = 0; i < tt->n; i++) {
+        if (w) memcpy(w + i * RW, tt->st[i].w, 8 * RW);
+        if (par) par[i] = tt->par[i];
+        if (key) key[i] = r_key(&h->G, &tt->st[i]);
+    }
+    return 0;
+}
+int ort_path(ort_handle* h, uint64_t* w, int cap) {
+    if (!h->done) return -1;
+    int t = h->nturns - 1;
+    int64_t r = h->winner_rank;
+    if (t + 1 > cap) return -2;
+    int len = t + 1;
+    for (; t >= 0; t--) { memcpy(w + t * RW, h->turns[t].st[r].w, 8 * RW); r = (int64_t)h->turns[t].par[r]; }
+    return len;
+}
+int ort_get_mt_state(ort_handle* h, uint32_t* out625) {
+    memcpy(out625, h->mt.mt, 624 * 4); out625[624] = (uint32_t)h->mt.idx; return 0;
+}

@@ -253,6 +253,7 @@ def _run_realistic(goal, width, seed, shuffle, players=2):
             'final': [[p.player_id, list(p.cards), list(p.bonus), list(p.gems), p.pts, p.saved]
                       for p in last.players],
             'path': [{'hash': s.hash, 'repr': repr(s), 'cur': s.current_player, 'turn': s.turn_number,
+                      'frt': s.final_round_triggered, 'frp': s.final_round_player,
                       'pool': list(s.gem_pool.available), 'visible': list(s.market.all_visible_cards()),
                       'players': [[p.player_id, list(p.cards), list(p.gems), p.pts, p.saved] for p in s.players]}
                      for s in sol],
@@ -265,42 +266,71 @@ def cmd_realistic(args):
     _dump(f'realistic_g{args.goal}_p{args.players}_{tag}_w{args.width}_s{args.seed}.json', res)
 
 
-def cmd_realistic_succ(_args):
-    """Ordered successor lists + hashes for realistic states (random walks)."""
+def _competitive_heuristic():
+    """The reference's multi_competitive_heuristic is a closure inside MultiPlayerState.solve
+    (src/solver.py:778-812); rebuild it from its code object (no reference file is modified)."""
+    import types
     import src.solver as S
+    for c in S.MultiPlayerState.solve.__code__.co_consts:
+        if isinstance(c, types.CodeType) and c.co_name == 'multi_competitive_heuristic':
+            return types.FunctionType(c, S.__dict__)
+    raise RuntimeError('closure not found')
+
+
+def _enc_mp(s):
+    return {'hash': s.hash, 'cur': s.current_player, 'turn': s.turn_number,
+            'frt': s.final_round_triggered, 'frp': s.final_round_player,
+            'pool': list(s.gem_pool.available),
+            'vis': [list(s.market.tier1_visible), list(s.market.tier2_visible), list(s.market.tier3_visible)],
+            'decklen': [len(s.market.tier1_deck), len(s.market.tier2_deck), len(s.market.tier3_deck)],
+            'players': [[p.player_id, list(p.cards), list(p.bonus), list(p.gems), p.pts, p.saved] for p in s.players],
+            'game_over': s.is_game_over()}
+
+
+def cmd_realistic_succ(_args):
+    """Ordered successor lists + hashes + competitive scores for realistic states (buy-biased walks)."""
+    import src.solver as S
+    heur = _competitive_heuristic()
     out = []
     rng = random.Random(3)
     for players in (2, 3, 4):
         gpc = {2: 4, 3: 5, 4: 7}[players]
-        for walk in range(25):
-            cfg = S.GameConfig(num_players=players, target_points=15, gems_per_color=gpc, infinite_resources=False)
+        for walk in range(60):
+            target = rng.choice((3, 6, 15))
+            cfg = S.GameConfig(num_players=players, target_points=target, gems_per_color=gpc, infinite_resources=False)
             st = S.MultiPlayerState.newgame(cfg, shuffle_market=bool(walk % 2), seed=walk)
             m = st.market
-            for depth in range(rng.randrange(1, 40)):
+            depth = rng.randrange(1, 60)
+            for _ in range(depth):
                 kids = list(st)
                 if not kids:
                     break
-                # bias toward buys so markets evolve
-                st = kids[rng.randrange(min(len(kids), 3))] if rng.random() < 0.5 else kids[rng.randrange(len(kids))]
+                buys = [k for k in kids if sum(len(p.cards) for p in k.players) > sum(len(p.cards) for p in st.players)]
+                st = rng.choice(buys) if buys and rng.random() < 0.7 else rng.choice(kids)
+                if st.is_game_over():
+                    break
             kids = list(st)
-            def enc(s):
-                return {'hash': s.hash, 'cur': s.current_player, 'turn': s.turn_number,
-                        'frt': s.final_round_triggered, 'frp': s.final_round_player,
-                        'pool': list(s.gem_pool.available),
-                        'vis': [list(s.market.tier1_visible), list(s.market.tier2_visible),
-                                list(s.market.tier3_visible)],
-                        'decklen': [len(s.market.tier1_deck), len(s.market.tier2_deck), len(s.market.tier3_deck)],
-                        'players': [[p.player_id, list(p.cards), list(p.bonus), list(p.gems), p.pts, p.saved]
-                                    for p in s.players]}
-            random.seed(17)
-            scores = None
-            out.append({'players': players, 'shuffle': bool(walk % 2), 'seed': walk,
+            scores = []
+            for k in kids:
+                random.seed(17)
+                scores.append(heur(k).hex())
+            out.append({'players': players, 'target': target, 'shuffle': bool(walk % 2), 'seed': walk,
                         'market0': {'t1': list(m.tier1_visible) + list(m.tier1_deck),
                                     't2': list(m.tier2_visible) + list(m.tier2_deck),
                                     't3': list(m.tier3_visible) + list(m.tier3_deck)},
-                        'state': enc(st), 'children': [enc(k) for k in kids], 'game_over': st.is_game_over(),
+                        'state': _enc_mp(st), 'children': [_enc_mp(k) for k in kids], 'scores_seed17': scores,
                         'winner': st.get_winner()})
     _dump('realistic_succ.json', out)
+
+
+def cmd_realistic_small(_args):
+    out = []
+    for goal, width, seed, shuffle, players in [(5, 500, 1, False, 2), (6, 300, 2, True, 2), (8, 2000, 3, True, 2),
+                                                  (4, 100, 4, False, 3), (6, 1000, 5, True, 2), (3, 50, 6, True, 4)]:
+        r = _run_realistic(goal, width, seed, shuffle, players)
+        print(goal, width, seed, shuffle, players, r['moves'], r['wall_s'])
+        out.append(r)
+    _dump('realistic_small.json', out)
 
 
 def main():
@@ -310,6 +340,7 @@ def main():
     sub.add_parser('solves_small')
     sub.add_parser('bfs')
     sub.add_parser('realistic_succ')
+    sub.add_parser('realistic_small')
     p = sub.add_parser('solve')
     p.add_argument('--goal', type=int, required=True)
     p.add_argument('--heur', required=True)
@@ -323,7 +354,8 @@ def main():
     p.add_argument('--shuffle', action='store_true')
     args = ap.parse_args()
     {'tables': cmd_tables, 'solve': cmd_solve, 'solves_small': cmd_solves_small, 'bfs': cmd_bfs,
-     'realistic': cmd_realistic, 'realistic_succ': cmd_realistic_succ}[args.cmd](args)
+     'realistic': cmd_realistic, 'realistic_succ': cmd_realistic_succ,
+     'realistic_small': cmd_realistic_small}[args.cmd](args)
 
 
 if __name__ == '__main__':

@@ -1,0 +1,91 @@
+"""Realistic-mode C oracle pinned against the reference's captures (CPU)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_c
+from conftest import golden
+from splendor_amd.realistic import (CardMarket, GameConfig, GemPool, MultiPlayerState, PlayerState, game_params,
+                                    pack_state, tier_lists)
+
+
+def state_from_fixture(fx, st, tiers0, target):
+    P = fx['players']
+    cfg = GameConfig(num_players=P, target_points=target, gems_per_color={2: 4, 3: 5, 4: 7}[P],
+                     infinite_resources=False)
+    players = tuple(PlayerState(p[0], tuple(p[1]), tuple(p[2]), tuple(p[3]), p[4], p[5]) for p in st['players'])
+    decks = [tuple(tiers0[t][len(tiers0[t]) - st['decklen'][t]:]) for t in range(3)]
+    market = CardMarket(tuple(st['vis'][0]), tuple(st['vis'][1]), tuple(st['vis'][2]), *decks)
+    return MultiPlayerState(cfg, players, GemPool(tuple(st['pool'])), market, st['cur'], st['turn'], st['frt'],
+                            st['frp'])
+
+
+def _tiers0(fx):
+    return [fx['market0']['t1'], fx['market0']['t2'], fx['market0']['t3']]
+
+
+def test_realistic_successors_hashes_scores():
+    n_children = 0
+    for fx in golden('realistic_succ.json'):
+        t0 = _tiers0(fx)
+        s = state_from_fixture(fx, fx['state'], t0, fx['target'])
+        assert s.hash == fx['state']['hash']          # host mirror hashes like the reference
+        params, tiers = game_params(s.config, t0)
+        w = pack_state(s, t0)
+        assert oracle_c.rt_key(params, tiers, w) == fx['state']['hash']
+        assert oracle_c.rt_game_over(params, tiers, w) == fx['state']['game_over']
+        kids, keys = oracle_c.rt_successors(params, tiers, w)
+        assert [oracle_c.to_signed(int(k)) for k in keys] == [c['hash'] for c in fx['children']]
+        exp = [pack_state(state_from_fixture(fx, c, t0, fx['target']), t0) for c in fx['children']]
+        assert len(kids) == len(exp)
+        for a, b in zip(kids, exp):
+            assert np.array_equal(a, b)
+        random.seed(17)
+        k = random.randint(1, 100)
+        for c, sc in zip(exp, fx['scores_seed17']):
+            assert oracle_c.rt_score(params, tiers, c, k).hex() == sc
+        n_children += len(kids)
+    assert n_children > 500
+
+
+def _solve_fixture(g):
+    cfg = GameConfig(num_players=g['players'], target_points=g['goal'],
+                     gems_per_color={2: 4, 3: 5, 4: 7}[g['players']], infinite_resources=False)
+    t0 = [g['market']['t1'], g['market']['t2'], g['market']['t3']]
+    assert tuple(map(tuple, t0)) == tuple(map(tuple, tier_lists(g['shuffle'], g['seed'] if g['shuffle'] else None)))
+    root = MultiPlayerState.newgame(cfg, shuffle_market=g['shuffle'], seed=g['seed'] if g['shuffle'] else None)
+    params, tiers = game_params(cfg, t0)
+    random.seed(g['seed'])
+    o = oracle_c.OracleRealistic(params, tiers, beam_width=g['beam_width'], mt_state625=random.getstate()[1],
+                                 root_w=pack_state(root, t0))
+    tr = o.run()
+    turns = [t for t in g['turns'] if t['n_unique'] > 0]   # the final sorted([]) after game over
+    done_turns = [t for t in tr if not t['done']]
+    assert len(done_turns) == len(turns)
+    for i, t in enumerate(turns):
+        _, _, key = o.turn_arrays(i + 1)
+        assert tr[i]['n_unique'] == t['n_unique'] and len(key) == t['n_kept']
+        assert oracle_c.beam_digest(key) == t['digest'], f'turn {i + 1}'
+    path = o.path()
+    assert [oracle_c.rt_key(params, tiers, w) for w in path] == [p['hash'] for p in g['path']]
+    assert oracle_c.mt_fingerprint(o.mt_state()) == g['final_mt']
+    o.close()
+
+
+def test_realistic_small_solves():
+    for g in golden('realistic_small.json'):
+        _solve_fixture(g)
+
+
+def test_realistic_readme_example():
+    """README.md:148-157 example: goal 6, unshuffled, W=3000, seed 0 -> 32 moves, P0 wins."""
+    g = golden('realistic_g6_p2_fixed_w3000_s0.json')
+    assert g['moves'] == 32 and g['winner'] == 0
+    _solve_fixture(g)
+
+
+@pytest.mark.slow
+def test_realistic_c4_scale_golden():
+    """Goal 15 --shuffle seed 0 W=20k (50 moves), the reference's own run."""
+    _solve_fixture(golden('realistic_g15_p2_shuf_w20000_s0.json'))
