@@ -163,6 +163,18 @@ int sbd_receive(sb_engine* e, const uint64_t* d_lo, const uint64_t* d_hi, const 
                 const uint64_t* d_key, int64_t n, int32_t heur);
 int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
 
+/* ---- realistic multi-player mode (MultiPlayerState, src/solver.py:471-860; config C4) ----
+ * params = {players (2..4), target_points, len tier1, len tier2, len tier3}; tiers = 3 x 40 int32
+ * card orders of the tiers (visible first 4, then the deck, src/solver.py:94-119); root_w = the
+ * 12-word packed root (oracle/csrc/oracle.c realistic section).  sb_destroy / sb_get_mt_state /
+ * sb_num_turns / sb_turn_size / sb_sync / sb_visited_size accept realistic handles. */
+int sbr_create(const sb_config* cfg, const int32_t* params, const int32_t* tiers, const uint32_t* mt_state625,
+               const uint64_t* root_w, sb_engine** out);
+/* one iteration of MultiPlayerState.solve's loop (src/solver.py:820-852) */
+int sbr_step(sb_engine* e, sb_step_stats* out);
+int sbr_read_turn(sb_engine* e, int32_t turn, int64_t start, int64_t n, uint64_t* w, uint32_t* par, uint64_t* key);
+int sbr_path(sb_engine* e, uint64_t* w, int32_t cap, int32_t* len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -464,6 +464,13 @@ static void build_patterns(Tables& T) {
 }
 
 // ------------------------------------------------------------------ engine
+// realistic-mode game constants (sb_realistic.inc)
+struct RGame {
+    int P, target;
+    int tlen[3];
+    uint8_t tier[3][40];
+};
+
 struct Turn {
     uint64_t* lo = nullptr;
     uint64_t* hi = nullptr;
@@ -510,6 +517,13 @@ struct Engine {
     int64_t ncand = 0, nuniq_local = 0, nkept_local = 0;
     int64_t goff = 0;
     int part_D = 1;
+    // realistic mode (mode 1): 12-word states in Turn::lo
+    int mode = 0;
+    RGame rgame_storage{};
+    RGame* rgame = nullptr;
+    uint32_t* d_rfirst = nullptr;
+    uint32_t* h_rfirst = nullptr;
+    DBuf<uint64_t> nw;
     DBuf<uint64_t> cand_key, cand_tag;
     DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
     DBuf<uint8_t> digit;
@@ -843,6 +857,10 @@ int sb_step(sb_engine* h, sb_step_stats* out) {
         set_error("sb_step: null argument");
         return SB_ERR_ARG;
     }
+    if (h->E.mode != 0) {
+        set_error("sb_step: realistic handle (use sbr_step)");
+        return SB_ERR_STATE;
+    }
     return guarded([&]() {
         SB_HIP(hipSetDevice(h->E.dev));
         engine_step(h->E, out);
@@ -982,6 +1000,9 @@ void sb_destroy(sb_engine* h) {
     noise_free(E.noise);
     if (E.tab) (void)hipFree(E.tab);
     if (E.own) (void)hipFree(E.own);
+    if (E.d_rfirst) (void)hipFree(E.d_rfirst);
+    if (E.h_rfirst) (void)hipHostFree(E.h_rfirst);
+    E.nw.release();
     E.cand_key.release();
     E.cand_tag.release();
     E.cand_ro.release();
@@ -1123,3 +1144,4 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
 }  // extern "C"
 
 #include "sb_dist.inc"
+#include "sb_realistic.inc"
