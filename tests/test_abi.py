@@ -12,7 +12,7 @@ HEADER = os.path.join(REPO, 'include', 'splendor_beam.h')
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:int|void|const char\*)\s+(sbd?_\w+)\s*\(', text, re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|void|const char\*)\s+(sb[dr]?_\w+)\s*\(', text, re.M)))
 
 
 def test_header_declares_expected_entry_points():
