@@ -8,12 +8,13 @@
 //                   src/solver.py:357-388) into an LDS child queue; the queue is then processed
 //                   densely (one child per lane): CPython tuple hash, visited-set probe/insert and
 //                   an atomicMin claim of the child's (turn, parent rank, ordinal) tag
-//   k_survive       a child survives iff its key was new this turn AND its tag won the claim:
-//                   exactly `if next_step in trail: continue` with first-occurrence order
-//                   (src/solver.py:446-450)
-//   scan            survivor counts -> next_queue offsets (parent rank, ordinal order)
-//   k_emit          survivors' packed states, parent links and heuristic scores; the noise of
-//                   next_queue element k is the k-th accepted MT19937 draw (sb_mt.hip)
+//                   — a claimant that displaces a same-turn holder marks it lost, so a child
+//                   survives iff it claimed and was never displaced: exactly
+//                   `if next_step in trail: continue` with first-occurrence order (src/solver.py:446-450)
+//   scan            survivor counts (cand & ~lost) -> next_queue offsets (parent rank, ordinal order)
+//   k_emit_q        survivors' packed states, parent links and heuristic scores, built densely from
+//                   an LDS queue; the noise of next_queue element k is the k-th accepted MT19937
+//                   draw (sb_mt.hip)
 //   top-k           stable descending sort + truncate (src/solver.py:452-456; sb_sort.hip)
 //   k_gather        the kept beam for the next turn + the per-pts first-rank table
 //
@@ -23,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -39,7 +41,7 @@ void set_error(const std::string& msg) { g_err = msg; }
 static Tables g_host_tables;
 static bool g_tables_ready = false;
 
-struct Entry {
+struct alignas(16) Entry {
     uint64_t key;
     uint64_t tag;
 };
@@ -71,6 +73,52 @@ __device__ __forceinline__ bool visit_claim(Entry* __restrict__ tab, uint64_t ma
     uint64_t cur = tab[h].tag;   // stale reads only over-estimate (EMPTY or a larger same-turn tag)
     if (cur != EMPTY && cur < tag) return false;   // seen in an earlier turn, or claimed earlier this turn
     atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+    return true;
+}
+
+// Claim with displacement marking (single-GPU speedrun path).  The winner of a key within a turn is
+// the smallest tag (parent rank, ordinal) — the reference's first occurrence in next_queue order.  A
+// claimant that lowers a same-turn tag marks the displaced holder in `lost`; one whose atomicMin finds
+// a smaller tag has lost itself.  Every duplicate is therefore resolved by exactly one of the two, and
+// once the grid drains the survivors are cand & ~lost — no second pass over the table.
+__device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t mask, uint64_t key, uint64_t tag,
+                                               unsigned long long* __restrict__ lost, uint32_t* err) {
+    uint64_t h = mix64(key) & mask;
+    uint64_t cur;   // the entry's tag; stale reads only over-estimate (tags only decrease)
+    for (int probe = 0;; probe++) {
+        const ulonglong2 ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);   // key and tag, one load
+        uint64_t k = ent.x;
+        if (k == EMPTY) {
+            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
+                                      (unsigned long long)key);
+            if (prev == EMPTY) {
+                cur = EMPTY;
+                break;
+            }
+            if (prev == key) {
+                cur = tab[h].tag;
+                break;
+            }
+            k = prev;
+        }
+        if (k == key) {
+            cur = ent.y;
+            break;
+        }
+        h = (h + 1) & mask;
+        if (probe >= MAX_PROBE) {
+            atomicOr(err, 1u);
+            return false;
+        }
+    }
+    if (cur != EMPTY && cur < tag) return false;
+    const uint64_t old = atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+    if (old < tag) return false;
+    if (old != EMPTY) {   // old > tag >= this turn's prefix: a same-turn holder, now displaced
+        const uint64_t ro = (old >> 8) & 0xFFFFFFFFull;
+        const uint32_t oo = (uint32_t)(old & 255);
+        atomicOr(&lost[ro * 3 + (oo >> 6)], 1ull << (oo & 63));
+    }
     return true;
 }
 
@@ -135,32 +183,49 @@ __device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* 
 
 // Parents [0, n); for each raw child: desc byte and visited-set slot at [rank*MAX_CHILDREN + ordinal],
 // candidate bitmask (3 x u64) per parent.
+// LM (lost marking): no desc / rslot rows; displaced same-turn claims are marked in `lost` instead.
+template <bool LM>
 __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
                                                   uint64_t mask, uint64_t turn_tag, uint8_t* __restrict__ desc,
                                                   uint32_t* __restrict__ rslot, unsigned long long* __restrict__ cand,
+                                                  unsigned long long* __restrict__ lost,
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err) {
     __shared__ XpShared S;
     load_tables_lds(T, S.card, S.pat, S.npat, S.mlo, S.mhi);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = lanemask_lt();
     if (t == 0) S.nraw = 0;
-    for (int64_t base = (int64_t)blockIdx.x * XP_PAR; base < n; base += (int64_t)gridDim.x * XP_PAR) {
+    // parent words of a group, one per thread (t < 16: lo, t < 32: hi), loaded a group ahead
+    auto fetch = [&](int64_t b) -> uint64_t {
+        const int64_t r = b + (t & (XP_PAR - 1));
+        if (t >= 2 * XP_PAR || r >= n) return 0ull;
+        return t < XP_PAR ? blo[r] : bhi[r];
+    };
+    int64_t base = (int64_t)blockIdx.x * XP_PAR;
+    uint64_t pf = base < n ? fetch(base) : 0ull;
+    for (; base < n; base += (int64_t)gridDim.x * XP_PAR) {
         if (t == 0) {
             S.nbuy = 0;
             S.ntake = 0;
         }
         if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
+        if (t < XP_PAR) S.plo[t] = pf;
+        else if (t < 2 * XP_PAR) S.phi[t - XP_PAR] = pf;
         __syncthreads();
+        {
+            const int64_t nb = base + (int64_t)gridDim.x * XP_PAR;
+            if (nb < n) pf = fetch(nb);
+        }
         // ---- phase A: each wave enumerates 4 parents (ballot compaction, canonical order)
         for (int s = w; s < XP_PAR; s += XP_NT / 64) {
             const int64_t r = base + s;
             if (r >= n) break;
-            const uint64_t lo = blo[r], hi = bhi[r];
+            const uint64_t lo = S.plo[s], hi = S.phi[s];
             Derived d;
             derive_lds(S.mlo, S.mhi, lo, hi, d);
             int ord = 0;
-            uint8_t* dr = desc + r * MAX_CHILDREN;
+            uint8_t* dr = LM ? nullptr : desc + r * MAX_CHILDREN;
 #pragma unroll
             for (int pass = 0; pass < 2; pass++) {   // buys, deck order (src/solver.py:369-374)
                 const int c = pass * 64 + lane;
@@ -173,7 +238,7 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
                 if (v) {
                     const int o = ord + pre;
                     S.qbuy[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)c << 12);
-                    dr[o] = (uint8_t)c;
+                    if constexpr (!LM) dr[o] = (uint8_t)c;
                 }
                 ord += cnt;
             }
@@ -192,14 +257,12 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
                     if (v) {
                         const int o = ord + pre;
                         S.qtake[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)(NCARDS + p) << 12);
-                        dr[o] = (uint8_t)(NCARDS + p);
+                        if constexpr (!LM) dr[o] = (uint8_t)(NCARDS + p);
                     }
                     ord += cnt;
                 }
             }
             if (lane == 0) {
-                S.plo[s] = lo;
-                S.phi[s] = hi;
                 S.prank[s] = r;
                 S.pbk[s] = bk;
                 atomicAdd(&S.nraw, (uint32_t)ord);
@@ -231,9 +294,14 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
             }
             const int64_t r = S.prank[s];
             const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
-            uint32_t slot;
-            const bool c = visit_claim(tab, mask, key, tag, &slot, err);
-            rslot[r * MAX_CHILDREN + o] = slot;
+            bool c;
+            if constexpr (LM) {
+                c = visit_claim_lm(tab, mask, key, tag, lost, err);
+            } else {
+                uint32_t slot;
+                c = visit_claim(tab, mask, key, tag, &slot, err);
+                rslot[r * MAX_CHILDREN + o] = slot;
+            }
             if (c) atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
         }
         __syncthreads();
@@ -330,6 +398,166 @@ __global__ __launch_bounds__(256) void k_emit(const Tables* __restrict__ T, cons
             }
             k += __popcll(sm);
         }
+    }
+}
+
+// ------------------------------------------------------------------ survivors of the lost-marking path
+__global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long long* __restrict__ cand,
+                                                  const unsigned long long* __restrict__ lost, uint32_t* __restrict__ cnt) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        cnt[r] = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
+                 __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
+}
+
+// rank of ordinal o among the set bits of the 192-bit mask (m0, m1, m2)
+__device__ __forceinline__ uint32_t mask_rank(uint64_t m0, uint64_t m1, uint64_t m2, int o) {
+    const uint64_t below = (1ull << (o & 63)) - 1;
+    if (o < 64) return __popcll(m0 & below);
+    if (o < 128) return __popcll(m0) + __popcll(m1 & below);
+    return __popcll(m0) + __popcll(m1) + __popcll(m2 & below);
+}
+__device__ __forceinline__ bool mask_bit(uint64_t m0, uint64_t m1, uint64_t m2, int o) {
+    const uint64_t m = o < 64 ? m0 : (o < 128 ? m1 : m2);
+    return (m >> (o & 63)) & 1;
+}
+
+// ------------------------------------------------------------------ k_emit_q (block queue, dense children)
+// Phase A: a wave per parent re-enumerates its children in canonical order and queues the survivors
+// (cand & ~lost) with their rank inside the parent.  Phase B: all threads build the queued children
+// densely — state, parent link, float64 score with the MT noise of its next_queue position.
+constexpr int EM_PAR = 32;
+struct EmShared {
+    uint32_t card[NCARDS];
+    uint32_t pat[4][NPAT_MAX];
+    int32_t npat[4];
+    uint64_t mlo[NCOL];
+    uint32_t mhi[NCOL];
+    uint64_t sm[EM_PAR][3];
+    uint64_t plo[EM_PAR], phi[EM_PAR];
+    uint32_t poff[EM_PAR];
+    int32_t pbk[EM_PAR];
+    uint32_t q[EM_PAR * MAX_CHILDREN];
+    uint32_t nq;
+};
+
+template <int H>
+__global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
+                                                const uint64_t* __restrict__ bhi, int64_t n,
+                                                const unsigned long long* __restrict__ cand,
+                                                const unsigned long long* __restrict__ lost,
+                                                const uint32_t* __restrict__ off, uint64_t* __restrict__ nlo,
+                                                uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
+                                                uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
+                                                uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
+                                                uint32_t* __restrict__ err) {
+    __shared__ EmShared S;
+    load_tables_lds(T, S.card, S.pat, S.npat, S.mlo, S.mhi);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint64_t lt = lanemask_lt();
+    // per-parent inputs of a group, one value per thread: t < 96 survivor masks, then lo, hi, off
+    auto fetch = [&](int64_t b) -> uint64_t {
+        if (t < 3 * EM_PAR) {
+            const int64_t i = b * 3 + t;
+            return i < n * 3 ? (uint64_t)(cand[i] & ~lost[i]) : 0ull;
+        }
+        const int j = t - 3 * EM_PAR, s = j & (EM_PAR - 1);
+        const int64_t r = b + s;
+        if (r >= n || j >= 3 * EM_PAR) return 0ull;
+        return j < EM_PAR ? blo[r] : (j < 2 * EM_PAR ? bhi[r] : (uint64_t)off[r]);
+    };
+    int64_t base = (int64_t)blockIdx.x * EM_PAR;
+    uint64_t pf = base < n ? fetch(base) : 0ull;
+    for (; base < n; base += (int64_t)gridDim.x * EM_PAR) {
+        if (t == 0) S.nq = 0;
+        if (t < 3 * EM_PAR) (&S.sm[0][0])[t] = pf;
+        else if (t < 6 * EM_PAR) {
+            const int j = t - 3 * EM_PAR, s = j & (EM_PAR - 1);
+            if (j < EM_PAR) S.plo[s] = pf;
+            else if (j < 2 * EM_PAR) S.phi[s] = pf;
+            else S.poff[s] = (uint32_t)pf;
+        }
+        __syncthreads();
+        const int64_t nb = base + (int64_t)gridDim.x * EM_PAR;
+        if (nb < n) pf = fetch(nb);   // next group's inputs load under this group's work
+        for (int s = w; s < EM_PAR; s += 4) {
+            const int64_t r = base + s;
+            if (r >= n) break;
+            const uint64_t m0 = S.sm[s][0], m1 = S.sm[s][1], m2 = S.sm[s][2];
+            if ((m0 | m1 | m2) == 0) continue;
+            const uint64_t lo = S.plo[s], hi = S.phi[s];
+            Derived d;
+            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            const int bk = take_bucket(d);
+            int ord = 0;
+#pragma unroll
+            for (int pass = 0; pass < 2; pass++) {   // buys, deck order
+                const int c = pass * 64 + lane;
+                const bool v = c < NCARDS && !st_owns(lo, hi, c) && affordable(S.card[c < NCARDS ? c : 0], d);
+                const uint64_t m = __ballot(v);
+                const int o = ord + __popcll(m & lt);
+                const bool sv = v && mask_bit(m0, m1, m2, o);
+                const uint64_t sm = __ballot(sv);
+                if (sm) {
+                    uint32_t qb = 0;
+                    if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)__popcll(sm));
+                    qb = __shfl(qb, 0, 64);
+                    if (sv)
+                        S.q[qb + __popcll(sm & lt)] = (uint32_t)s | ((uint32_t)c << 5) | (mask_rank(m0, m1, m2, o) << 13);
+                }
+                ord += __popcll(m);
+            }
+            if (bk >= 0) {   // takes, pattern order
+                const int np = S.npat[bk];
+                for (int p0 = 0; p0 < np; p0 += 64) {
+                    const int p = p0 + lane;
+                    uint32_t gf;
+                    const bool v = p < np && take_child(S.pat[bk][p < np ? p : 0], d, &gf);
+                    const uint64_t m = __ballot(v);
+                    const int o = ord + __popcll(m & lt);
+                    const bool sv = v && mask_bit(m0, m1, m2, o);
+                    const uint64_t sm = __ballot(sv);
+                    if (sm) {
+                        uint32_t qb = 0;
+                        if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)__popcll(sm));
+                        qb = __shfl(qb, 0, 64);
+                        if (sv)
+                            S.q[qb + __popcll(sm & lt)] =
+                                (uint32_t)s | ((uint32_t)(NCARDS + p) << 5) | (mask_rank(m0, m1, m2, o) << 13);
+                    }
+                    ord += __popcll(m);
+                }
+            }
+            if (lane == 0) S.pbk[s] = bk;
+        }
+        __syncthreads();
+        const uint32_t nq = S.nq;
+        for (uint32_t i = t; i < nq; i += 256) {
+            const uint32_t e = S.q[i];
+            const int s = (int)(e & 31), dsc = (int)((e >> 5) & 255);
+            const uint32_t kk = S.poff[s] + (e >> 13);
+            int nv = 1;
+            if constexpr (H >= 0) nv = ring[(ring_base + kk) & ring_mask];
+            const uint64_t lo = S.plo[s], hi = S.phi[s];
+            Derived d;
+            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            uint64_t clo = lo, chi;
+            if (dsc < NCARDS) {
+                chi = buy_child_hi(S.card[dsc], dsc, d, hi, &clo);
+            } else {
+                uint32_t gf;
+                take_child(S.pat[S.pbk[s]][dsc - NCARDS], d, &gf);
+                chi = st_with_gems(hi, gf);
+            }
+            nlo[kk] = clo;
+            nhi[kk] = chi;
+            npar[kk] = par_base + (uint32_t)(base + s);
+            if constexpr (H >= 0) {
+                if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
+                const double sc = score_of<H>(T->pw, *T, clo, chi, T->noise[nv - 1]);
+                skey[kk] = (uint64_t)__double_as_longlong(sc);
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -495,7 +723,7 @@ struct Engine {
     std::vector<Turn> turns;
     DBuf<uint8_t> desc;
     DBuf<uint32_t> rslot;
-    DBuf<unsigned long long> cand, surv;
+    DBuf<unsigned long long> cand, surv, lost;
     DBuf<uint32_t> cnt, off;
     DBuf<uint64_t> nlo, nhi, skey;
     DBuf<uint32_t> npar, kidx;
@@ -510,6 +738,8 @@ struct Engine {
     bool done = false;
     int64_t winner_rank = -1;
     int max_pts = 0;
+    uint64_t last_nu = 0;
+    Arena turn_mem;
     hipEvent_t ev[8] = {};
     // distributed mode (world_size > 1): owner shard of the global visited set + exchange staging
     Entry* own = nullptr;
@@ -598,22 +828,23 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     }
     const bool heur = E.cfg.use_heuristic != 0;
     // speculative noise for this step (side stream, overlaps expansion)
-    if (heur && E.noise.produced - E.noise.consumed < (uint64_t)n * 12) noise_generate_async(E.noise, E.s_mt);
+    // keep about two steps of accepted draws ahead of the consumer
+    if (heur && E.noise.produced - E.noise.consumed < std::max<uint64_t>((uint64_t)n * 12, 2 * E.last_nu + (uint64_t)n))
+        noise_generate_async(E.noise, E.s_mt);
 
     if (timing) SB_HIP(hipEventRecord(E.ev[0], E.s));
-    E.desc.ensure((size_t)n * MAX_CHILDREN);
-    E.rslot.ensure((size_t)n * MAX_CHILDREN);
     E.cand.ensure((size_t)n * 3);
-    E.surv.ensure((size_t)n * 3);
+    E.lost.ensure((size_t)n * 3);
     E.cnt.ensure((size_t)n);
     E.off.ensure((size_t)n);
     SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
+    SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
-    hipLaunchKernelGGL(k_expand, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo, cur.hi,
-                       n, E.tab, E.tab_mask, turn_tag, E.desc.p, E.rslot.p, E.cand.p, E.d_nraw, E.d_small + 1);
+    hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
+                       cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr, E.cand.p,
+                       E.lost.p, E.d_nraw, E.d_small + 1);
     if (timing) SB_HIP(hipEventRecord(E.ev[1], E.s));
-    hipLaunchKernelGGL(k_survive, dim3(grid_cap(n, 4, 1u << 16)), dim3(256), 0, E.s, n, E.tab, turn_tag, E.rslot.p,
-                       E.cand.p, E.surv.p, E.cnt.p);
+    hipLaunchKernelGGL(k_count_lm, dim3(grid_cap(n, 256, 1u << 14)), dim3(256), 0, E.s, n, E.cand.p, E.lost.p, E.cnt.p);
     scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
     if (timing) SB_HIP(hipEventRecord(E.ev[2], E.s));
     SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 8, hipMemcpyDeviceToHost, E.s));
@@ -639,23 +870,24 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     E.npar.ensure(nu);
     if (heur) {
         E.skey.ensure(nu);
-        float t0 = 0;
-        (void)t0;
+        const auto t0 = std::chrono::steady_clock::now();
         noise_ensure(E.noise, (uint64_t)nu, E.s_mt);
+        out->ms_sort = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        E.last_nu = (uint64_t)nu;
     }
     if (timing) SB_HIP(hipEventRecord(E.ev[3], E.s));
-    const unsigned eg = grid_cap(n, 4, 1u << 16);
+    const unsigned eg = grid_cap(n, EM_PAR, 1u << 15);
     const uint64_t rbase = E.noise.consumed;
     if (!heur) {
-        hipLaunchKernelGGL(k_emit<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p,
-                           E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,
-                           0u, E.d_small + 1);
+        hipLaunchKernelGGL(k_emit_q<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,
+                           E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask,
+                           rbase, 0u, E.d_small + 1);
     } else {
         switch (E.cfg.heuristic) {
-#define EMIT(H)                                                                                                     \
-    hipLaunchKernelGGL(k_emit<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.desc.p, E.surv.p, \
-                       E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase,    \
-                       0u, E.d_small + 1);                                                                          \
+#define EMIT(H)                                                                                                   \
+    hipLaunchKernelGGL(k_emit_q<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,        \
+                       E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
+                       rbase, 0u, E.d_small + 1);                                                                 \
     break;
             case 1: EMIT(1)
             case 2: EMIT(2)
@@ -676,9 +908,9 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     }
     if (timing) SB_HIP(hipEventRecord(E.ev[5], E.s));
     Turn nt;
-    SB_HIP(hipMalloc((void**)&nt.lo, m * 8));
-    SB_HIP(hipMalloc((void**)&nt.hi, m * 8));
-    SB_HIP(hipMalloc((void**)&nt.par, m * 4));
+    nt.lo = (uint64_t*)E.turn_mem.alloc(m * 8);
+    nt.hi = (uint64_t*)E.turn_mem.alloc(m * 8);
+    nt.par = (uint32_t*)E.turn_mem.alloc(m * 4);
     nt.n = m;
     SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
     hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
@@ -696,6 +928,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         out->ms_emit = ev_ms(E.ev[3], E.ev[4]);
         out->ms_select = ev_ms(E.ev[4], E.ev[5]);
         out->ms_gather = ev_ms(E.ev[5], E.ev[6]);
+        out->ms_mt = ev_ms(E.ev[2], E.ev[3]);   // host round trip for n_unique + any wait on the noise stream
         out->ms_total = ev_ms(E.ev[0], E.ev[6]);
     }
 }
@@ -787,6 +1020,10 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
     int rc = guarded([&]() {
         Engine& E = h->E;
         E.cfg = *cfg;
+        {   // turn storage blocks of about four beams
+            const int64_t wl = cfg->beam_width / std::max(1, (int)cfg->world_size) + 1;
+            E.turn_mem.block_bytes = std::max<size_t>((size_t)256 << 20, (size_t)wl * 4 * 20);
+        }
         E.dev = cfg->device;
         SB_HIP(hipSetDevice(E.dev));
         SB_HIP(hipStreamCreateWithFlags(&E.s, hipStreamNonBlocking));
@@ -820,9 +1057,9 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         SB_HIP(hipMemsetAsync(E.d_small, 0, 264 * 4, E.s));
         // root: turn 0, visited = {root}
         Turn t0;
-        SB_HIP(hipMalloc((void**)&t0.lo, 8));
-        SB_HIP(hipMalloc((void**)&t0.hi, 8));
-        SB_HIP(hipMalloc((void**)&t0.par, 4));
+        t0.lo = (uint64_t*)E.turn_mem.alloc(8);
+        t0.hi = (uint64_t*)E.turn_mem.alloc(8);
+        t0.par = (uint32_t*)E.turn_mem.alloc(4);
         uint32_t nopar = 0xFFFFFFFFu;
         SB_HIP(hipMemcpyAsync(t0.lo, &root_lo, 8, hipMemcpyHostToDevice, E.s));
         SB_HIP(hipMemcpyAsync(t0.hi, &root_hi, 8, hipMemcpyHostToDevice, E.s));
@@ -970,11 +1207,7 @@ void sb_destroy(sb_engine* h) {
     (void)hipSetDevice(E.dev);
     if (E.s) (void)hipStreamSynchronize(E.s);
     if (E.s_mt) (void)hipStreamSynchronize(E.s_mt);
-    for (auto& t : E.turns) {
-        (void)hipFree(t.lo);
-        (void)hipFree(t.hi);
-        (void)hipFree(t.par);
-    }
+    E.turn_mem.release();
     E.desc.release();
     E.rslot.release();
     E.cand.release();

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 namespace sb {
 
@@ -29,7 +30,7 @@ struct DBuf {
     void ensure(size_t n) {
         if (n <= cap) return;
         if (p) SB_HIP(hipFree(p));
-        size_t c = n < 1024 ? 1024 : n;
+        size_t c = n < 1024 ? 1024 : n + n / 2;   // slack: a growing size reallocates rarely
         SB_HIP(hipMalloc((void**)&p, c * sizeof(T)));
         cap = c;
     }
@@ -37,6 +38,36 @@ struct DBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+    }
+};
+
+// Bump allocator for the per-turn beams (kept for path reconstruction until sb_destroy): no
+// hipMalloc on the step path — hipMalloc/hipFree can serialise against in-flight work.
+struct Arena {
+    std::vector<void*> blocks;
+    char* cur = nullptr;
+    size_t left = 0;
+    size_t block_bytes = (size_t)256 << 20;
+    void* alloc(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        if (bytes > left) {
+            const size_t b = bytes > block_bytes ? bytes : block_bytes;
+            void* p = nullptr;
+            SB_HIP(hipMalloc(&p, b));
+            blocks.push_back(p);
+            cur = (char*)p;
+            left = b;
+        }
+        void* r = cur;
+        cur += bytes;
+        left -= bytes;
+        return r;
+    }
+    void release() {
+        for (void* p : blocks) (void)hipFree(p);
+        blocks.clear();
+        cur = nullptr;
+        left = 0;
     }
 };
 

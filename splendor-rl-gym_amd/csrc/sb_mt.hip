@@ -309,7 +309,8 @@ static void noise_collect(NoiseStream& ns) {
 }
 
 void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st) {
-    noise_collect(ns);
+    // wait for an in-flight chunk only when its draws are needed now
+    if (ns.pending && (ns.produced - ns.consumed < need || hipEventQuery(ns.ev_ready) == hipSuccess)) noise_collect(ns);
     if (need > ns.ring_mask + 1 - noise_chunk_words(ns))
         throw HipError{hipErrorOutOfMemory, "noise ring too small for one step"};
     while (ns.produced - ns.consumed < need) {
