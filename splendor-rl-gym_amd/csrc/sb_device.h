@@ -33,6 +33,11 @@ enum PowRow { P03 = 0, P04, P05, P06, P07, P08, P12, P20, P25, P28, P32 };
 
 // Card word: bits 0..14 cost (3 bits per colour), 15..17 pt, 18..20 colour.
 // Pattern word: bits 0..14 (delta + 2) per colour, 15..17 index of the 2 in a take-2 pattern (7 = take-3).
+// Enumeration tables (derived on the host from the same deck and patterns):
+//   aff_lo/aff_hi[i][v]  cards whose colour-i cost is <= v (90-bit masks): the buy set of a state is
+//                        AND_i aff[i][min(g_i + b_i, 7)] minus its own cards, in deck order
+//   pdelta[b][p]         pattern p of bucket b as a packed signed gem delta: child gems = gf + pdelta
+//   tmask[gf]            valid take patterns (bucket order) of gem field gf, 100-bit mask
 struct Tables {
     uint32_t card[NCARDS];
     uint32_t pat[4][NPAT_MAX];
@@ -41,6 +46,10 @@ struct Tables {
     uint32_t colmask_hi[NCOL];
     double pw[N_POW][POW_BASES];
     double noise[100];
+    uint64_t aff_lo[NCOL][8];
+    uint32_t aff_hi[NCOL][8];
+    int32_t pdelta[4][NPAT_MAX];
+    uint64_t tmask[1 << 15][2];
 };
 
 // ---------------------------------------------------------------- state codec
@@ -184,19 +193,10 @@ __device__ __forceinline__ int take_bucket(const Derived& d) {
 
 // ---------------------------------------------------------------- scores (src/solver.py:210-286)
 // pw is the host-captured float(x) ** e table; evaluation order is Python's, left to right.
+// G = total gems, B = total bonus (== len(cards) in speedrun), U = colours with a bonus.
 template <int H>
-__device__ __forceinline__ double score_of(const double (*pw)[POW_BASES], const Tables& T, uint64_t lo, uint64_t hi,
-                                           double noise) {
-    uint32_t chi = st_chi(hi);
-    int G = 0, B = 0, U = 0;
-#pragma unroll
-    for (int i = 0; i < NCOL; i++) {
-        int b = __popcll(lo & T.colmask_lo[i]) + __popc(chi & T.colmask_hi[i]);
-        G += st_gem(hi, i);
-        B += b;
-        U += b > 0;
-    }
-    int pts = st_pts(hi), saved = st_saved(hi);
+__device__ __forceinline__ double score_vals(const double (*pw)[POW_BASES], int pts, int saved, int G, int B, int U,
+                                             double noise) {
     saved = saved < POW_BASES ? saved : POW_BASES - 1;   // guarded on the host: saved < 256 asserted
     if constexpr (H == 0) {   // simple
         return pw[P04][saved] * pw[P25][pts] + noise;
@@ -219,6 +219,54 @@ __device__ __forceinline__ double score_of(const double (*pw)[POW_BASES], const 
         r = r + pw[P08][U] * 10;
         return r + noise;
     }
+}
+
+template <int H>
+__device__ __forceinline__ double score_of(const double (*pw)[POW_BASES], const Tables& T, uint64_t lo, uint64_t hi,
+                                           double noise) {
+    uint32_t chi = st_chi(hi);
+    int G = 0, B = 0, U = 0;
+#pragma unroll
+    for (int i = 0; i < NCOL; i++) {
+        int b = __popcll(lo & T.colmask_lo[i]) + __popc(chi & T.colmask_hi[i]);
+        G += st_gem(hi, i);
+        B += b;
+        U += b > 0;
+    }
+    return score_vals<H>(pw, st_pts(hi), st_saved(hi), G, B, U, noise);
+}
+
+// ---------------------------------------------------------------- mask enumeration
+// buy set of a state in deck order: (lo 64 cards, hi 26 cards)
+__device__ __forceinline__ void buy_set(const uint64_t (*aff_lo)[8], const uint32_t (*aff_hi)[8], const Derived& d,
+                                        uint64_t lo, uint64_t hi, uint64_t* blo, uint32_t* bhi) {
+    uint64_t ml = ~lo;
+    uint32_t mh = ~st_chi(hi) & ((1u << 26) - 1);
+#pragma unroll
+    for (int i = 0; i < NCOL; i++) {
+        int v = d.g[i] + d.b[i];
+        v = v < MAXG ? v : MAXG;
+        ml &= aff_lo[i][v];
+        mh &= aff_hi[i][v];
+    }
+    *blo = ml;
+    *bhi = mh;
+}
+// per-colour bonus counts packed 5 bits each
+__device__ __forceinline__ uint32_t pack_bonus(const Derived& d) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < NCOL; i++) p |= (uint32_t)d.b[i] << (5 * i);
+    return p;
+}
+__device__ __forceinline__ void derive_packed(uint64_t hi, uint32_t pbon, Derived& d) {
+#pragma unroll
+    for (int i = 0; i < NCOL; i++) {
+        d.g[i] = st_gem(hi, i);
+        d.b[i] = (int)((pbon >> (5 * i)) & 31);
+    }
+    d.pts = st_pts(hi);
+    d.saved = st_saved(hi);
 }
 
 }  // namespace sb

@@ -146,18 +146,36 @@ constexpr int XP_PAR = 16;            // parents per block iteration (4 per wave
 
 struct XpShared {
     uint32_t card[NCARDS];
-    uint32_t pat[4][NPAT_MAX];
-    int32_t npat[4];
+    int32_t pdelta[4][NPAT_MAX];
     uint64_t mlo[NCOL];
     uint32_t mhi[NCOL];
+    uint64_t alo[NCOL][8];
+    uint32_t ahi[NCOL][8];
     uint64_t plo[XP_PAR], phi[XP_PAR], phc[XP_PAR];
-    int64_t prank[XP_PAR];
+    uint64_t ptm[XP_PAR][2];
+    uint64_t pbl[XP_PAR];
+    uint32_t pbh[XP_PAR];
+    uint32_t pbon[XP_PAR];
     int32_t pbk[XP_PAR];
     unsigned long long cmask[XP_PAR][3];
-    uint32_t qbuy[XP_PAR * NCARDS];
-    uint32_t qtake[XP_PAR * NPAT_MAX];
-    uint32_t nbuy, ntake, nraw;
+    uint32_t q[XP_PAR * MAX_CHILDREN];
+    uint32_t nq, nraw;
 };
+
+// enumeration tables into LDS: cards, colour masks, affordability masks, pattern deltas
+__device__ __forceinline__ void load_enum_lds(const Tables* __restrict__ T, uint32_t* card, uint64_t* mlo, uint32_t* mhi,
+                                              uint64_t (*alo)[8], uint32_t (*ahi)[8], int32_t (*pdelta)[NPAT_MAX]) {
+    for (int i = threadIdx.x; i < NCARDS; i += blockDim.x) card[i] = T->card[i];
+    for (int i = threadIdx.x; i < 4 * NPAT_MAX; i += blockDim.x) (&pdelta[0][0])[i] = (&T->pdelta[0][0])[i];
+    for (int i = threadIdx.x; i < NCOL * 8; i += blockDim.x) {
+        (&alo[0][0])[i] = (&T->aff_lo[0][0])[i];
+        (&ahi[0][0])[i] = (&T->aff_hi[0][0])[i];
+    }
+    if (threadIdx.x < NCOL) {
+        mlo[threadIdx.x] = T->colmask_lo[threadIdx.x];
+        mhi[threadIdx.x] = T->colmask_hi[threadIdx.x];
+    }
+}
 
 __device__ __forceinline__ void load_tables_lds(const Tables* __restrict__ T, uint32_t* card, uint32_t (*pat)[NPAT_MAX],
                                                 int32_t* npat, uint64_t* mlo, uint32_t* mhi) {
@@ -181,9 +199,12 @@ __device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* 
     d.saved = st_saved(hi);
 }
 
-// Parents [0, n); for each raw child: desc byte and visited-set slot at [rank*MAX_CHILDREN + ordinal],
-// candidate bitmask (3 x u64) per parent.
-// LM (lost marking): no desc / rslot rows; displaced same-turn claims are marked in `lost` instead.
+// Parents [0, n): every raw child is probed/claimed in the visited set; candidate bitmask (3 x u64)
+// per parent.  Successor order (src/solver.py:357-388) comes from masks: the buy set in deck order
+// (AND of per-colour affordability masks minus owned cards), then the valid take patterns of the
+// gem field in bucket order (Tables::tmask) — ordinal = rank in that order.
+// LM (lost marking): displaced same-turn claims are marked in `lost`; otherwise (sharded path) each
+// raw child's desc byte and visited slot are written at [rank*MAX_CHILDREN + ordinal].
 template <bool LM>
 __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
@@ -192,7 +213,7 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
                                                   unsigned long long* __restrict__ lost,
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err) {
     __shared__ XpShared S;
-    load_tables_lds(T, S.card, S.pat, S.npat, S.mlo, S.mhi);
+    load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = lanemask_lt();
     if (t == 0) S.nraw = 0;
@@ -205,10 +226,7 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
     int64_t base = (int64_t)blockIdx.x * XP_PAR;
     uint64_t pf = base < n ? fetch(base) : 0ull;
     for (; base < n; base += (int64_t)gridDim.x * XP_PAR) {
-        if (t == 0) {
-            S.nbuy = 0;
-            S.ntake = 0;
-        }
+        if (t == 0) S.nq = 0;
         if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
         if (t < XP_PAR) S.plo[t] = pf;
         else if (t < 2 * XP_PAR) S.phi[t - XP_PAR] = pf;
@@ -217,82 +235,75 @@ __global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, 
             const int64_t nb = base + (int64_t)gridDim.x * XP_PAR;
             if (nb < n) pf = fetch(nb);
         }
-        // ---- phase A: each wave enumerates 4 parents (ballot compaction, canonical order)
+        // prologue, a lane per parent: buy set, bucket, take mask, packed bonus, hash of the card tuple
+        if (t < XP_PAR) {
+            const uint64_t lo = S.plo[t], hi = S.phi[t];
+            Derived d;
+            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            uint64_t bl;
+            uint32_t bh;
+            buy_set(S.alo, S.ahi, d, lo, hi, &bl, &bh);
+            const int bk = take_bucket(d);
+            uint64_t t0 = 0, t1 = 0;
+            if (bk >= 0) {
+                const uint32_t gf = st_gemfield(hi);
+                t0 = T->tmask[gf][0];
+                t1 = T->tmask[gf][1];
+            }
+            S.pbl[t] = bl;
+            S.pbh[t] = bh;
+            S.ptm[t][0] = t0;
+            S.ptm[t][1] = t1;
+            S.pbon[t] = pack_bonus(d);
+            S.pbk[t] = bk;
+        } else if (t < 2 * XP_PAR) {
+            const int s = t - XP_PAR;
+            S.phc[s] = hash_cards(S.plo[s], st_chi(S.phi[s]));
+        }
+        __syncthreads();
+        // ---- phase A: a wave per parent lays its children out in canonical order
         for (int s = w; s < XP_PAR; s += XP_NT / 64) {
             const int64_t r = base + s;
             if (r >= n) break;
-            const uint64_t lo = S.plo[s], hi = S.phi[s];
-            Derived d;
-            derive_lds(S.mlo, S.mhi, lo, hi, d);
-            int ord = 0;
-            uint8_t* dr = LM ? nullptr : desc + r * MAX_CHILDREN;
-#pragma unroll
-            for (int pass = 0; pass < 2; pass++) {   // buys, deck order (src/solver.py:369-374)
-                const int c = pass * 64 + lane;
-                const bool v = c < NCARDS && !st_owns(lo, hi, c) && affordable(S.card[c < NCARDS ? c : 0], d);
-                const uint64_t m = __ballot(v);
-                const int pre = __popcll(m & lt), cnt = __popcll(m);
-                uint32_t qb = 0;
-                if (lane == 0 && cnt) qb = atomicAdd(&S.nbuy, (uint32_t)cnt);
-                qb = __shfl(qb, 0, 64);
-                if (v) {
-                    const int o = ord + pre;
-                    S.qbuy[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)c << 12);
-                    if constexpr (!LM) dr[o] = (uint8_t)c;
-                }
-                ord += cnt;
-            }
-            const int bk = take_bucket(d);
-            if (bk >= 0) {   // takes, pattern order (src/solver.py:381-388, src/gems.py:85-108)
-                const int np = S.npat[bk];
-                for (int p0 = 0; p0 < np; p0 += 64) {
-                    const int p = p0 + lane;
-                    uint32_t gf;
-                    const bool v = p < np && take_child(S.pat[bk][p < np ? p : 0], d, &gf);
-                    const uint64_t m = __ballot(v);
-                    const int pre = __popcll(m & lt), cnt = __popcll(m);
-                    uint32_t qb = 0;
-                    if (lane == 0 && cnt) qb = atomicAdd(&S.ntake, (uint32_t)cnt);
-                    qb = __shfl(qb, 0, 64);
-                    if (v) {
-                        const int o = ord + pre;
-                        S.qtake[qb + pre] = (uint32_t)s | ((uint32_t)o << 4) | ((uint32_t)(NCARDS + p) << 12);
-                        if constexpr (!LM) dr[o] = (uint8_t)(NCARDS + p);
-                    }
-                    ord += cnt;
-                }
-            }
+            const uint64_t bl = S.pbl[s], t0 = S.ptm[s][0], t1 = S.ptm[s][1];
+            const uint32_t bh = S.pbh[s];
+            const int nbl = __popcll(bl), nb = nbl + __popc(bh), nt0 = __popcll(t0);
+            const int tot = nb + nt0 + __popcll(t1);
+            uint32_t qb = 0;
             if (lane == 0) {
-                S.prank[s] = r;
-                S.pbk[s] = bk;
-                atomicAdd(&S.nraw, (uint32_t)ord);
+                qb = atomicAdd(&S.nq, (uint32_t)tot);
+                atomicAdd(&S.nraw, (uint32_t)tot);
             }
+            qb = __shfl(qb, 0, 64);
+            uint8_t* dr = LM ? nullptr : desc + r * MAX_CHILDREN;
+            auto put = [&](int o, int dsc) {
+                S.q[qb + o] = (uint32_t)s | ((uint32_t)o << 5) | ((uint32_t)dsc << 13);
+                if constexpr (!LM) dr[o] = (uint8_t)dsc;
+            };
+            if ((bl >> lane) & 1) put(__popcll(bl & lt), lane);
+            if (lane < 26 && ((bh >> lane) & 1)) put(nbl + __popc(bh & (uint32_t)lt), 64 + lane);
+            if ((t0 >> lane) & 1) put(nb + __popcll(t0 & lt), NCARDS + lane);
+            if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
         }
         __syncthreads();
-        // ---- parent prologue: hash(cards) of each parent, one lane each
-        if (t < XP_PAR && base + t < n) S.phc[t] = hash_cards(S.plo[t], st_chi(S.phi[t]));
-        __syncthreads();
-        // ---- phase B: dense child processing, buys first (uniform hash loops), then takes
-        const uint32_t nb = S.nbuy, tot = nb + S.ntake;
-        for (uint32_t i = t; i < tot; i += XP_NT) {
-            const uint32_t e = i < nb ? S.qbuy[i] : S.qtake[i - nb];
-            const int s = (int)(e & 15), o = (int)((e >> 4) & 255), dsc = (int)(e >> 12);
+        // ---- phase B: dense child processing: key, visited probe + claim
+        const uint32_t nq = S.nq;
+        for (uint32_t i = t; i < nq; i += XP_NT) {
+            const uint32_t e = S.q[i];
+            const int s = (int)(e & 31), o = (int)((e >> 5) & 255), dsc = (int)(e >> 13);
             const uint64_t lo = S.plo[s], hi = S.phi[s];
             uint64_t key;
             if (dsc < NCARDS) {
                 Derived d;
-                derive_lds(S.mlo, S.mhi, lo, hi, d);
+                derive_packed(hi, S.pbon[s], d);
                 uint64_t clo = lo;
                 const uint64_t chi = buy_child_hi(S.card[dsc], dsc, d, hi, &clo);
                 key = state_key(hash_cards(clo, st_chi(chi)), hash_gems(st_gemfield(chi)));
             } else {
-                Derived d;
-                derive_lds(S.mlo, S.mhi, lo, hi, d);
-                uint32_t gf;
-                take_child(S.pat[S.pbk[s]][dsc - NCARDS], d, &gf);
+                const uint32_t gf = (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]);
                 key = state_key(S.phc[s], hash_gems(gf));
             }
-            const int64_t r = S.prank[s];
+            const int64_t r = base + s;
             const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
             bool c;
             if constexpr (LM) {
@@ -428,13 +439,18 @@ __device__ __forceinline__ bool mask_bit(uint64_t m0, uint64_t m1, uint64_t m2, 
 constexpr int EM_PAR = 32;
 struct EmShared {
     uint32_t card[NCARDS];
-    uint32_t pat[4][NPAT_MAX];
-    int32_t npat[4];
+    int32_t pdelta[4][NPAT_MAX];
     uint64_t mlo[NCOL];
     uint32_t mhi[NCOL];
+    uint64_t alo[NCOL][8];
+    uint32_t ahi[NCOL][8];
     uint64_t sm[EM_PAR][3];
     uint64_t plo[EM_PAR], phi[EM_PAR];
+    uint64_t ptm[EM_PAR][2];
+    uint64_t pbl[EM_PAR];
+    uint32_t pbh[EM_PAR];
     uint32_t poff[EM_PAR];
+    uint32_t pbon[EM_PAR];
     int32_t pbk[EM_PAR];
     uint32_t q[EM_PAR * MAX_CHILDREN];
     uint32_t nq;
@@ -451,7 +467,7 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
                                                 uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
                                                 uint32_t* __restrict__ err) {
     __shared__ EmShared S;
-    load_tables_lds(T, S.card, S.pat, S.npat, S.mlo, S.mhi);
+    load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = lanemask_lt();
     // per-parent inputs of a group, one value per thread: t < 96 survivor masks, then lo, hi, off
@@ -477,59 +493,56 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
             else S.poff[s] = (uint32_t)pf;
         }
         __syncthreads();
-        const int64_t nb = base + (int64_t)gridDim.x * EM_PAR;
-        if (nb < n) pf = fetch(nb);   // next group's inputs load under this group's work
+        const int64_t nb_ = base + (int64_t)gridDim.x * EM_PAR;
+        if (nb_ < n) pf = fetch(nb_);   // next group's inputs load under this group's work
+        // prologue, a lane per parent with survivors: buy set, bucket, take mask, packed bonus
+        if (t < EM_PAR && (S.sm[t][0] | S.sm[t][1] | S.sm[t][2])) {
+            const uint64_t lo = S.plo[t], hi = S.phi[t];
+            Derived d;
+            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            uint64_t bl;
+            uint32_t bh;
+            buy_set(S.alo, S.ahi, d, lo, hi, &bl, &bh);
+            const int bk = take_bucket(d);
+            uint64_t t0 = 0, t1 = 0;
+            if (bk >= 0) {
+                const uint32_t gf = st_gemfield(hi);
+                t0 = T->tmask[gf][0];
+                t1 = T->tmask[gf][1];
+            }
+            S.pbl[t] = bl;
+            S.pbh[t] = bh;
+            S.ptm[t][0] = t0;
+            S.ptm[t][1] = t1;
+            S.pbon[t] = pack_bonus(d);
+            S.pbk[t] = bk;
+        }
+        __syncthreads();
+        // ---- phase A: a wave per parent queues its surviving children with their rank
         for (int s = w; s < EM_PAR; s += 4) {
             const int64_t r = base + s;
             if (r >= n) break;
             const uint64_t m0 = S.sm[s][0], m1 = S.sm[s][1], m2 = S.sm[s][2];
             if ((m0 | m1 | m2) == 0) continue;
-            const uint64_t lo = S.plo[s], hi = S.phi[s];
-            Derived d;
-            derive_lds(S.mlo, S.mhi, lo, hi, d);
-            const int bk = take_bucket(d);
-            int ord = 0;
-#pragma unroll
-            for (int pass = 0; pass < 2; pass++) {   // buys, deck order
-                const int c = pass * 64 + lane;
-                const bool v = c < NCARDS && !st_owns(lo, hi, c) && affordable(S.card[c < NCARDS ? c : 0], d);
-                const uint64_t m = __ballot(v);
-                const int o = ord + __popcll(m & lt);
-                const bool sv = v && mask_bit(m0, m1, m2, o);
-                const uint64_t sm = __ballot(sv);
-                if (sm) {
-                    uint32_t qb = 0;
-                    if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)__popcll(sm));
-                    qb = __shfl(qb, 0, 64);
-                    if (sv)
-                        S.q[qb + __popcll(sm & lt)] = (uint32_t)s | ((uint32_t)c << 5) | (mask_rank(m0, m1, m2, o) << 13);
+            const uint64_t bl = S.pbl[s], t0 = S.ptm[s][0], t1 = S.ptm[s][1];
+            const uint32_t bh = S.pbh[s];
+            const int nbl = __popcll(bl), nb = nbl + __popc(bh), nt0 = __popcll(t0);
+            uint32_t qb = 0;
+            if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2)));
+            qb = __shfl(qb, 0, 64);
+            auto put = [&](int o, int dsc) {
+                if (mask_bit(m0, m1, m2, o)) {
+                    const uint32_t rk = mask_rank(m0, m1, m2, o);
+                    S.q[qb + rk] = (uint32_t)s | ((uint32_t)dsc << 5) | (rk << 13);
                 }
-                ord += __popcll(m);
-            }
-            if (bk >= 0) {   // takes, pattern order
-                const int np = S.npat[bk];
-                for (int p0 = 0; p0 < np; p0 += 64) {
-                    const int p = p0 + lane;
-                    uint32_t gf;
-                    const bool v = p < np && take_child(S.pat[bk][p < np ? p : 0], d, &gf);
-                    const uint64_t m = __ballot(v);
-                    const int o = ord + __popcll(m & lt);
-                    const bool sv = v && mask_bit(m0, m1, m2, o);
-                    const uint64_t sm = __ballot(sv);
-                    if (sm) {
-                        uint32_t qb = 0;
-                        if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)__popcll(sm));
-                        qb = __shfl(qb, 0, 64);
-                        if (sv)
-                            S.q[qb + __popcll(sm & lt)] =
-                                (uint32_t)s | ((uint32_t)(NCARDS + p) << 5) | (mask_rank(m0, m1, m2, o) << 13);
-                    }
-                    ord += __popcll(m);
-                }
-            }
-            if (lane == 0) S.pbk[s] = bk;
+            };
+            if ((bl >> lane) & 1) put(__popcll(bl & lt), lane);
+            if (lane < 26 && ((bh >> lane) & 1)) put(nbl + __popc(bh & (uint32_t)lt), 64 + lane);
+            if ((t0 >> lane) & 1) put(nb + __popcll(t0 & lt), NCARDS + lane);
+            if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
         }
         __syncthreads();
+        // ---- phase B: build the queued children densely
         const uint32_t nq = S.nq;
         for (uint32_t i = t; i < nq; i += 256) {
             const uint32_t e = S.q[i];
@@ -539,21 +552,31 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
             if constexpr (H >= 0) nv = ring[(ring_base + kk) & ring_mask];
             const uint64_t lo = S.plo[s], hi = S.phi[s];
             Derived d;
-            derive_lds(S.mlo, S.mhi, lo, hi, d);
+            derive_packed(hi, S.pbon[s], d);
+            int B = 0, U = 0;
+#pragma unroll
+            for (int c = 0; c < NCOL; c++) {
+                B += d.b[c];
+                U += d.b[c] > 0;
+            }
             uint64_t clo = lo, chi;
             if (dsc < NCARDS) {
-                chi = buy_child_hi(S.card[dsc], dsc, d, hi, &clo);
+                const uint32_t cw = S.card[dsc];
+                chi = buy_child_hi(cw, dsc, d, hi, &clo);
+                B += 1;
+                U += d.b[card_color(cw)] == 0;
             } else {
-                uint32_t gf;
-                take_child(S.pat[S.pbk[s]][dsc - NCARDS], d, &gf);
-                chi = st_with_gems(hi, gf);
+                chi = st_with_gems(hi, (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]));
             }
             nlo[kk] = clo;
             nhi[kk] = chi;
             npar[kk] = par_base + (uint32_t)(base + s);
             if constexpr (H >= 0) {
                 if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
-                const double sc = score_of<H>(T->pw, *T, clo, chi, T->noise[nv - 1]);
+                int G = 0;
+#pragma unroll
+                for (int c = 0; c < NCOL; c++) G += st_gem(chi, c);
+                const double sc = score_vals<H>(T->pw, st_pts(chi), st_saved(chi), G, B, U, T->noise[nv - 1]);
                 skey[kk] = (uint64_t)__double_as_longlong(sc);
             }
         }
@@ -689,6 +712,45 @@ static void build_patterns(Tables& T) {
     add(3, {1, -1, 0, 0, 0}, false);
     add(3, {2, -1, -1, 0, 0}, true);
     add(3, {2, -2, 0, 0, 0}, true);
+}
+
+// masks and packed deltas for mask enumeration (see Tables); restates affordable() / take_child()
+static void build_enum_tables(Tables& T) {
+    for (int i = 0; i < NCOL; i++)
+        for (int v = 0; v < 8; v++) {
+            T.aff_lo[i][v] = 0;
+            T.aff_hi[i][v] = 0;
+            for (int c = 0; c < NCARDS; c++)
+                if ((int)((T.card[c] >> (3 * i)) & 7) <= v) {
+                    if (c < 64) T.aff_lo[i][v] |= 1ull << c;
+                    else T.aff_hi[i][v] |= 1u << (c - 64);
+                }
+        }
+    for (int b = 0; b < 4; b++)
+        for (int p = 0; p < NPAT_MAX; p++) {
+            int32_t dl = 0;
+            if (p < T.npat[b])
+                for (int i = NCOL - 1; i >= 0; i--) dl = dl * 8 + ((int)((T.pat[b][p] >> (3 * i)) & 7) - 2);
+            T.pdelta[b][p] = dl;
+        }
+    for (int gf = 0; gf < (1 << 15); gf++) {
+        int g[NCOL], tot = 0;
+        for (int i = 0; i < NCOL; i++) tot += g[i] = (gf >> (3 * i)) & 7;
+        T.tmask[gf][0] = T.tmask[gf][1] = 0;
+        const int bk = tot > 10 ? -1 : (tot <= 7 ? 0 : tot - 7);
+        if (bk < 0) continue;
+        for (int p = 0; p < T.npat[bk]; p++) {
+            const uint32_t w = T.pat[bk][p];
+            const int two = (int)((w >> 15) & 7);
+            bool ok = true;
+            for (int i = 0; i < NCOL; i++) {
+                const int x = g[i] + (int)((w >> (3 * i)) & 7) - 2;
+                ok &= x >= 0 && x <= MAXG;
+                if (two == i) ok &= g[i] <= MAXG - 4;
+            }
+            if (ok) T.tmask[gf][p >> 6] |= 1ull << (p & 63);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ engine
@@ -988,6 +1050,7 @@ int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const dou
         else T.colmask_hi[r[6]] |= 1u << (c - 64);
     }
     build_patterns(T);
+    build_enum_tables(T);
     memcpy(T.pw, pow_tables, sizeof T.pw);
     memcpy(T.noise, noise, sizeof T.noise);
     (void)npat_host;
@@ -1220,16 +1283,7 @@ void sb_destroy(sb_engine* h) {
     E.npar.release();
     E.kidx.release();
     E.scan.tiles.release();
-    E.topk.k0.release();
-    E.topk.k1.release();
-    E.topk.v0.release();
-    E.topk.v1.release();
-    E.topk.tile_hist.release();
-    E.topk.tile_a.release();
-    E.topk.tile_b.release();
-    E.topk.small.release();
-    E.topk.scan.tiles.release();
-    if (E.topk.h_flags) (void)hipHostFree(E.topk.h_flags);
+    E.topk.release();
     noise_free(E.noise);
     if (E.tab) (void)hipFree(E.tab);
     if (E.own) (void)hipFree(E.own);
@@ -1359,16 +1413,7 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
         SB_HIP(hipMemcpy(out_idx, di, m * 4, hipMemcpyDeviceToHost));
         SB_HIP(hipFree(dk));
         SB_HIP(hipFree(di));
-        s.k0.release();
-        s.k1.release();
-        s.v0.release();
-        s.v1.release();
-        s.tile_hist.release();
-        s.tile_a.release();
-        s.tile_b.release();
-        s.small.release();
-        s.scan.tiles.release();
-        if (s.h_flags) (void)hipHostFree(s.h_flags);
+        s.release();
         SB_HIP(hipStreamDestroy(st));
         return SB_OK;
     });

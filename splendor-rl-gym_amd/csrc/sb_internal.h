@@ -86,11 +86,13 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* 
 struct TopkScratch {
     DBuf<uint64_t> k0, k1;          // keys ping-pong
     DBuf<uint32_t> v0, v1;          // payload ping-pong
+    DBuf<uint64_t> ck;              // select candidates (keys)
+    DBuf<uint32_t> ci;              // select candidates (indices)
     DBuf<uint32_t> tile_hist;       // 256 x ntiles
-    DBuf<uint32_t> tile_a, tile_b;  // compaction counts
-    DBuf<uint64_t> small;           // select state + global histograms
-    uint32_t* h_flags = nullptr;    // pinned
+    DBuf<uint32_t> tile_a, tile_b;  // partition counts
+    DBuf<uint64_t> small;           // select state + histogram
     ScanScratch scan;
+    void release();
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.
 // Returns the number written (min(n, keep)).  ms_select/ms_sort get device times if non-null.

@@ -1,12 +1,21 @@
-// sb_sort.hip — stable descending top-k of u64 score keys: the device form of
+// sb_sort.hip — stable descending top-k of u64 keys: the device form of
 //   queue = sorted(next_queue, key=heuristic, reverse=True)[:beam_width]   (src/solver.py:452-456)
-// sorted() is stable, so ties keep next_queue order (element index).  Scores are positive
-// float64, so their IEEE bit patterns order like the values.
+// sorted() is stable, so ties keep next_queue order (element index).  Keys are order-preserving u64
+// images of the float64 scores (positive scores: the IEEE bits themselves).
 //
-//   1. radix select (MSB-first 8-bit digits) finds the threshold bucket holding the keep-th key
-//      and how many of its elements (first in index order) are kept;
-//   2. an order-preserving compaction writes the kept (key, index) pairs in index order;
-//   3. a stable LSD radix sort on ~key orders them; passes whose digit is constant are skipped.
+// Everything runs on the stream without a host round trip:
+//   1. min/max of the keys: bits above the highest differing bit are common to all keys and skipped;
+//   2. one 11-bit MSB radix-select pass over all n keys finds the bucket holding the keep-th key;
+//   3. an order-preserving partition writes the keys above that bucket (all kept) to the output and
+//      the bucket's elements to a candidate buffer — later passes read only the candidates;
+//   4. further 11-bit passes on the candidates resolve the threshold key T and how many of its ties
+//      (first in index order) are kept; a final partition appends the candidates above T, then those
+//      ties.  The three output groups have disjoint key sets, so a stable sort of the concatenation
+//      orders ties by index exactly as sorted() does;
+//   5. a stable LSD radix sort (8-bit digits) on ~key orders the kept set; digits above the highest
+//      bit that differs inside [lowest kept key, max] are constant and skipped on the device.
+#include <algorithm>
+
 #include "sb_block.h"
 #include "sb_internal.h"
 
@@ -15,74 +24,146 @@ namespace sb {
 constexpr int TK_NT = 256;
 constexpr int TK_IPT = 16;
 constexpr int TK_TILE = TK_NT * TK_IPT;   // 4096
+constexpr int SEL_D = 11;                 // select digit bits
+constexpr int SEL_BINS = 1 << SEL_D;
+constexpr int SEL_PASSES_C = 6;           // candidate passes: ceil(64 / 11) upper bound
 
-// select state (device, u64 words): [0] prefix  [1] bits resolved  [2] need  [3] done
-//                                  [4..4+256) pass histogram   [260..260+8*256) global digit hists
-constexpr int SEL_HIST = 4;
-constexpr int GH = 260;
+// device state (u64 words)
+enum : int {
+    ST_MIN = 0, ST_MAX, ST_PREFIX, ST_SH, ST_NEED, ST_DONE,
+    ST_A,       // keys above the first bucket (kept, output group 1)
+    ST_NC,      // candidates (first bucket)
+    ST_G2,      // candidates above T (output group 2)
+    ST_E2,      // candidates equal to the resolved prefix (before the tie limit)
+    ST_BASE2,   // output offset of group 2 (= A)
+    ST_BASE3,   // output offset of group 3 (= A + G2)
+    ST_TOPK,    // sort: bits [0, TOPK) vary among the kept keys
+    ST_HIST = 16,
+    ST_WORDS = ST_HIST + SEL_BINS
+};
 
-__global__ void k_sel_init(uint64_t* st, int64_t keep) {
-    int t = threadIdx.x;
+__device__ __forceinline__ uint64_t hi_bits(uint64_t k, uint64_t sh) { return sh >= 64 ? 0ull : k >> sh; }
+
+__global__ void k_tk_init(uint64_t* st, int64_t keep) {
+    const int t = threadIdx.x;
+    if (t < ST_HIST) st[t] = 0;
+    __syncthreads();
     if (t == 0) {
-        st[0] = 0;
-        st[1] = 0;
-        st[2] = (uint64_t)keep;
-        st[3] = 0;
+        st[ST_MIN] = ~0ull;
+        st[ST_NEED] = (uint64_t)keep;
     }
-    for (int i = t; i < 256 + 8 * 256; i += blockDim.x) st[SEL_HIST + i] = 0;
+    for (int i = t; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
 }
 
-__global__ __launch_bounds__(TK_NT) void k_sel_hist(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
-    if (st[3]) return;
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+__global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
+    __shared__ unsigned long long smin, smax;
+    if (threadIdx.x == 0) {
+        smin = ~0ull;
+        smax = 0;
+    }
     __syncthreads();
-    const uint64_t prefix = st[0];
-    const int bits = (int)st[1];
+    uint64_t lo = ~0ull, hi = 0;
     for (int64_t i = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * TK_NT) {
-        uint64_t k = keys[i];
-        bool match = bits == 0 || (k >> (64 - bits)) == prefix;
-        if (match) atomicAdd(&h[(k >> (56 - bits)) & 255], 1u);
+        const uint64_t k = keys[i];
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+    atomicMin(&smin, (unsigned long long)lo);
+    atomicMax(&smax, (unsigned long long)hi);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMin((unsigned long long*)&st[ST_MIN], smin);
+        atomicMax((unsigned long long*)&st[ST_MAX], smax);
+    }
+}
+
+// common high bits of all keys: SH = position above the highest differing bit
+__global__ void k_tk_setup(uint64_t* st) {
+    const uint64_t x = st[ST_MIN] ^ st[ST_MAX];
+    const uint64_t top = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
+    st[ST_SH] = top;
+    st[ST_PREFIX] = hi_bits(st[ST_MIN], top);
+    st[ST_DONE] = top == 0;   // all keys equal: the first `keep` in index order
+}
+
+// histogram of the next digit over the elements matching the resolved prefix; n from n_dev if given
+__global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
+                                                   const uint64_t* __restrict__ n_dev, uint64_t* st) {
+    if (st[ST_DONE]) return;
+    __shared__ uint32_t h[TK_NT / 64][SEL_BINS];
+    const int w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < (TK_NT / 64) * SEL_BINS; i += TK_NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+    const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
+    const uint64_t d = sh < SEL_D ? sh : SEL_D;
+    const uint64_t dmask = (1ull << d) - 1;
+    for (int64_t i = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * TK_NT) {
+        const uint64_t k = keys[i];
+        if (hi_bits(k, sh) == prefix) atomicAdd(&h[w][(k >> (sh - d)) & dmask], 1u);
     }
     __syncthreads();
-    uint32_t c = h[threadIdx.x];
-    if (c) atomicAdd((unsigned long long*)&st[SEL_HIST + threadIdx.x], (unsigned long long)c);
-}
-
-__global__ void k_sel_pick(uint64_t* st) {
-    if (st[3] || threadIdx.x != 0) return;
-    uint64_t need = st[2], cum = 0;
-    int d = 255;
-    for (; d > 0; d--) {
-        uint64_t c = st[SEL_HIST + d];
-        if (cum + c >= need) break;
-        cum += c;
+    for (int b = threadIdx.x; b < SEL_BINS; b += TK_NT) {
+        const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
+        if (c) atomicAdd((unsigned long long*)&st[ST_HIST + b], (unsigned long long)c);
     }
-    uint64_t c = st[SEL_HIST + d];
-    need -= cum;
-    st[0] = (st[0] << 8) | (uint64_t)d;
-    st[1] += 8;
-    st[2] = need;
-    if (c == need || st[1] == 64) st[3] = 1;
-    for (int i = 0; i < 256; i++) st[SEL_HIST + i] = 0;
 }
 
-// tile counts of keys strictly above / equal to the threshold prefix
-__global__ __launch_bounds__(TK_NT) void k_sel_count(const uint64_t* __restrict__ keys, int64_t n,
-                                                      const uint64_t* __restrict__ st, uint32_t* __restrict__ gt,
-                                                      uint32_t* __restrict__ eq) {
+// pick the bucket holding the need-th largest matching element; clears the histogram
+__global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st) {
+    if (st[ST_DONE]) return;
     __shared__ uint32_t lds[TK_NT / 64 + 1];
-    const uint64_t prefix = st[0];
-    const int bits = (int)st[1];
+    const int t = threadIdx.x;
+    const uint64_t sh = st[ST_SH];
+    const uint64_t d = sh < SEL_D ? sh : SEL_D;
+    const int nb = 1 << d;
+    constexpr int PER = SEL_BINS / TK_NT;   // 8 bins per thread, descending
+    uint64_t c[PER];
+    uint64_t loc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int b = nb - 1 - (t * PER + j);
+        c[j] = b >= 0 ? st[ST_HIST + b] : 0;
+        loc += c[j];
+    }
+    // counts fit in u32 (n < 2^32)
+    uint32_t tot;
+    uint64_t cum = block_excl_scan<TK_NT>((uint32_t)loc, lds, &tot);
+    const uint64_t need = st[ST_NEED];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int b = nb - 1 - (t * PER + j);
+        if (b >= 0 && c[j] && cum < need && cum + c[j] >= need) {
+            const uint64_t nneed = need - cum;
+            st[ST_NEED] = nneed;
+            st[ST_PREFIX] = (st[ST_PREFIX] << d) | (uint64_t)b;
+            st[ST_SH] = sh - d;
+            st[ST_DONE] = (c[j] == nneed) || (sh - d == 0);
+        }
+        cum += c[j];
+    }
+    for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
+}
+
+// per-tile counts of elements above / equal to the resolved prefix
+__global__ __launch_bounds__(TK_NT) void k_tk_count(const uint64_t* __restrict__ keys, int64_t n_host,
+                                                    const uint64_t* __restrict__ n_dev, const uint64_t* __restrict__ st,
+                                                    uint32_t* __restrict__ gt, uint32_t* __restrict__ eq) {
+    __shared__ uint32_t lds[TK_NT / 64 + 1];
+    const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+    const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
     const int64_t base = (int64_t)blockIdx.x * TK_TILE;
     uint32_t a = 0, b = 0;
+    if (base < n) {
 #pragma unroll
-    for (int j = 0; j < TK_IPT; j++) {
-        int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
-        if (i < n) {
-            uint64_t top = keys[i] >> (64 - bits);
-            a += top > prefix;
-            b += top == prefix;
+        for (int j = 0; j < TK_IPT; j++) {
+            const int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
+            if (i < n) {
+                const uint64_t hb = hi_bits(keys[i], sh);
+                a += hb > prefix;
+                b += hb == prefix;
+            }
         }
     }
     uint32_t ta, tb;
@@ -94,75 +175,79 @@ __global__ __launch_bounds__(TK_NT) void k_sel_count(const uint64_t* __restrict_
     }
 }
 
-// single workgroup: eq -> exclusive eq offsets; gt -> exclusive kept offsets
-__global__ __launch_bounds__(1024) void k_sel_scan(uint32_t* __restrict__ gt, uint32_t* __restrict__ eq, int64_t ntiles,
-                                                    const uint64_t* __restrict__ st) {
+// single workgroup: exclusive tile offsets for both classes; totals into st[slot_gt], st[slot_eq].
+// phase 2 also sets the output bases of groups 2 and 3.
+__global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uint32_t* __restrict__ eq, int64_t ntiles,
+                                                   uint64_t* st, int slot_gt, int slot_eq, int phase2) {
     __shared__ uint32_t lds[1024 / 64 + 1];
-    const uint64_t m = st[2];
-    uint32_t ceq = 0, ckept = 0;
+    uint32_t cg = 0, ce = 0;
     for (int64_t b = 0; b < ntiles; b += 1024) {
-        int64_t i = b + threadIdx.x;
-        uint32_t g = i < ntiles ? gt[i] : 0, e = i < ntiles ? eq[i] : 0;
-        uint32_t te;
-        uint32_t ex_e = block_excl_scan<1024>(e, lds, &te) + ceq;
-        uint64_t take = ex_e >= m ? 0 : (m - ex_e < e ? m - ex_e : e);
-        uint32_t kept = g + (uint32_t)take, tk;
-        uint32_t ex_k = block_excl_scan<1024>(kept, lds, &tk) + ckept;
+        const int64_t i = b + threadIdx.x;
+        const uint32_t g = i < ntiles ? gt[i] : 0, e = i < ntiles ? eq[i] : 0;
+        uint32_t tg, te;
+        const uint32_t xg = block_excl_scan<1024>(g, lds, &tg) + cg;
+        const uint32_t xe = block_excl_scan<1024>(e, lds, &te) + ce;
         if (i < ntiles) {
-            eq[i] = ex_e;
-            gt[i] = ex_k;
+            gt[i] = xg;
+            eq[i] = xe;
         }
-        ceq += te;
-        ckept += tk;
+        cg += tg;
+        ce += te;
+    }
+    if (threadIdx.x == 0) {
+        st[slot_gt] = cg;
+        st[slot_eq] = ce;
+        if (phase2) {
+            st[ST_BASE2] = st[ST_A];
+            st[ST_BASE3] = st[ST_A] + cg;
+        }
     }
 }
 
-__global__ __launch_bounds__(TK_NT) void k_sel_write(const uint64_t* __restrict__ keys, int64_t n,
-                                                      const uint64_t* __restrict__ st, const uint32_t* __restrict__ kept_off,
-                                                      const uint32_t* __restrict__ eq_off, uint64_t* __restrict__ okeys,
-                                                      uint32_t* __restrict__ oidx) {
+// Order-preserving partition of a tile (striped loads, a workgroup scan per 256-element round):
+// elements above the prefix -> (gk, gi) at *gbase + rank; equal ones -> (ek, ei) at *ebase + rank,
+// only the first *limit of them if limit is given.
+__global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                                                    int64_t n_host, const uint64_t* __restrict__ n_dev,
+                                                    const uint64_t* __restrict__ st, const uint32_t* __restrict__ gt_off,
+                                                    const uint32_t* __restrict__ eq_off, uint64_t* __restrict__ gk,
+                                                    uint32_t* __restrict__ gi, const uint64_t* __restrict__ gbase,
+                                                    uint64_t* __restrict__ ek, uint32_t* __restrict__ ei,
+                                                    const uint64_t* __restrict__ ebase, const uint64_t* __restrict__ limit) {
     __shared__ uint32_t lds[TK_NT / 64 + 1];
-    const uint64_t prefix = st[0];
-    const int bits = (int)st[1];
-    const uint64_t m = st[2];
-    const int64_t base = (int64_t)blockIdx.x * TK_TILE + (int64_t)threadIdx.x * TK_IPT;   // blocked order
-    uint64_t k[TK_IPT];
-    uint32_t ne = 0;
-#pragma unroll
+    const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+    const int64_t base = (int64_t)blockIdx.x * TK_TILE;
+    if (base >= n) return;
+    const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
+    const uint64_t lim = limit ? *limit : ~0ull;
+    uint64_t og = (gbase ? *gbase : 0) + gt_off[blockIdx.x];
+    uint64_t re = eq_off[blockIdx.x];   // rank among equal elements
+    const uint64_t eb = ebase ? *ebase : 0;
     for (int j = 0; j < TK_IPT; j++) {
-        int64_t i = base + j;
-        k[j] = i < n ? keys[i] : 0;
-        uint64_t top = k[j] >> (64 - bits);
-        ne += (i < n) & (top == prefix);
-    }
-    uint32_t t;
-    uint32_t eq_run = block_excl_scan<TK_NT>(ne, lds, &t) + eq_off[blockIdx.x];
-    // kept count of this thread depends on eq_run; compute then scan
-    uint32_t kc = 0;
-    {
-        uint32_t er = eq_run;
-#pragma unroll
-        for (int j = 0; j < TK_IPT; j++) {
-            int64_t i = base + j;
-            if (i >= n) break;
-            uint64_t top = k[j] >> (64 - bits);
-            if (top > prefix) kc++;
-            else if (top == prefix) { kc += er < m; er++; }
+        const int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
+        uint64_t k = 0;
+        uint32_t fg = 0, fe = 0;
+        if (i < n) {
+            k = keys[i];
+            const uint64_t hb = hi_bits(k, sh);
+            fg = hb > prefix;
+            fe = hb == prefix;
         }
-    }
-    uint32_t out = block_excl_scan<TK_NT>(kc, lds, &t) + kept_off[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < TK_IPT; j++) {
-        int64_t i = base + j;
-        if (i >= n) break;
-        uint64_t top = k[j] >> (64 - bits);
-        bool keep = top > prefix;
-        if (top == prefix) { keep = eq_run < m; eq_run++; }
-        if (keep) {
-            okeys[out] = k[j];
-            oidx[out] = (uint32_t)i;
-            out++;
+        uint32_t tg, te;
+        const uint32_t rg = block_excl_scan<TK_NT>(fg, lds, &tg);
+        const uint32_t rv = block_excl_scan<TK_NT>(fe, lds, &te);
+        if (fg || fe) {
+            const uint32_t v = idx ? idx[i] : (uint32_t)i;
+            if (fg) {
+                gk[og + rg] = k;
+                gi[og + rg] = v;
+            } else if (re + rv < lim) {
+                ek[eb + re + rv] = k;
+                ei[eb + re + rv] = v;
+            }
         }
+        og += tg;
+        re += te;
     }
 }
 
@@ -173,39 +258,27 @@ __global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64
     }
 }
 
-// global digit histograms of ~key for all 8 LSD passes (constant-digit detection)
-__global__ __launch_bounds__(TK_NT) void k_sort_ghist(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
-    __shared__ uint32_t h[8][256];
-    for (int i = threadIdx.x; i < 8 * 256; i += TK_NT) (&h[0][0])[i] = 0;
-    __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * TK_NT) {
-        uint64_t k = ~keys[i];
-#pragma unroll
-        for (int p = 0; p < 8; p++) atomicAdd(&h[p][(k >> (8 * p)) & 255], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 8 * 256; i += TK_NT) {
-        uint32_t c = (&h[0][0])[i];
-        if (c) atomicAdd((unsigned long long*)&st[GH + i], (unsigned long long)c);
-    }
+// bits that vary among the kept keys: [lowest kept, max]; lowest kept >= prefix << sh
+__global__ void k_tk_sortsetup(uint64_t* st, int selected) {
+    uint64_t lo = st[ST_MIN];
+    if (selected) lo = st[ST_SH] >= 64 ? 0ull : (st[ST_PREFIX] << st[ST_SH]);
+    const uint64_t x = lo ^ st[ST_MAX];
+    st[ST_TOPK] = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
 }
 
-__global__ void k_sort_flags(const uint64_t* st, int64_t n, uint32_t* flags) {
-    int p = threadIdx.x;   // 8 threads
-    if (p >= 8) return;
-    uint32_t constant = 0;
-    for (int d = 0; d < 256; d++)
-        if (st[GH + p * 256 + d] == (uint64_t)n) constant = 1;
-    flags[p] = constant;
-}
+__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] + 7) / 8); }
 
-// per-tile histogram of digit (~key >> shift) & 255, column-major [digit][tile]
-__global__ __launch_bounds__(TK_NT) void k_sort_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
+// per-tile histogram of digit (~key >> 8p) & 255, column-major [digit][tile]; pass p reads buffer p & 1
+__global__ __launch_bounds__(TK_NT) void k_sort_hist(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ k1,
+                                                      int64_t n, int p, const uint64_t* __restrict__ st,
                                                       uint32_t* __restrict__ hist, int64_t ntiles) {
+    if (p >= sort_passes(st)) return;
+    const uint64_t* keys = (p & 1) ? k1 : k0;
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * TK_TILE;
+    const int shift = 8 * p;
 #pragma unroll
     for (int j = 0; j < TK_IPT; j++) {
         int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
@@ -217,10 +290,16 @@ __global__ __launch_bounds__(TK_NT) void k_sort_hist(const uint64_t* __restrict_
 
 // stable scatter: tile elements processed in index order, rank among equal digits by
 // wave match (8 ballots) + per-wave LDS counts.
-__global__ __launch_bounds__(TK_NT) void k_sort_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                         uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                         int64_t n, int shift, const uint32_t* __restrict__ hist,
-                                                         int64_t ntiles) {
+__global__ __launch_bounds__(TK_NT) void k_sort_scatter(uint64_t* __restrict__ k0, uint32_t* __restrict__ v0,
+                                                         uint64_t* __restrict__ k1, uint32_t* __restrict__ v1,
+                                                         int64_t n, int p, const uint64_t* __restrict__ st,
+                                                         const uint32_t* __restrict__ hist, int64_t ntiles) {
+    if (p >= sort_passes(st)) return;
+    const uint64_t* kin = (p & 1) ? k1 : k0;
+    const uint32_t* vin = (p & 1) ? v1 : v0;
+    uint64_t* kout = (p & 1) ? k0 : k1;
+    uint32_t* vout = (p & 1) ? v0 : v1;
+    const int shift = 8 * p;
     __shared__ uint32_t base_d[256];
     __shared__ uint32_t wcnt[TK_NT / 64][256];
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -256,7 +335,8 @@ __global__ __launch_bounds__(TK_NT) void k_sort_scatter(const uint64_t* __restri
     }
 }
 
-__global__ void k_copy_idx(const uint32_t* in, uint32_t* out, int64_t n) {
+__global__ void k_copy_idx(const uint32_t* v0, const uint32_t* v1, const uint64_t* st, uint32_t* out, int64_t n) {
+    const uint32_t* in = (sort_passes(st) & 1) ? v1 : v0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = in[i];
 }
@@ -267,6 +347,20 @@ static unsigned grid_for(int64_t n, int nt, unsigned cap = 8192) {
     return (unsigned)(g < cap ? g : cap);
 }
 
+void TopkScratch::release() {
+    k0.release();
+    k1.release();
+    v0.release();
+    v1.release();
+    ck.release();
+    ci.release();
+    tile_hist.release();
+    tile_a.release();
+    tile_b.release();
+    small.release();
+    scan.tiles.release();
+}
+
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
                          hipStream_t st) {
     if (n <= 0 || keep <= 0) return 0;
@@ -275,45 +369,58 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.k1.ensure(m);
     s.v0.ensure(m);
     s.v1.ensure(m);
-    s.small.ensure(GH + 8 * 256);
-    if (!s.h_flags) SB_HIP(hipHostMalloc((void**)&s.h_flags, 64, hipHostMallocDefault));
+    s.small.ensure(ST_WORDS);
     uint64_t* stv = s.small.p;
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m);
-    if (n > keep) {
-        for (int pass = 0; pass < 8; pass++) {
-            hipLaunchKernelGGL(k_sel_hist, dim3(grid_for(n, TK_NT * 8, 4096)), dim3(TK_NT), 0, st, keys, n, stv);
-            hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(64), 0, st, stv);
-        }
-        int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
+    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m);
+    hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
+    const bool selected = n > keep;
+    if (selected) {
+        const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
         s.tile_a.ensure(ntiles);
         s.tile_b.ensure(ntiles);
-        hipLaunchKernelGGL(k_sel_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, n, stv, s.tile_a.p, s.tile_b.p);
-        hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv);
-        hipLaunchKernelGGL(k_sel_write, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, n, stv, s.tile_a.p,
-                           s.tile_b.p, s.k0.p, s.v0.p);
+        s.ck.ensure(n);
+        s.ci.ensure(n);
+        const unsigned hg = grid_for(n, TK_NT * 16, 2048);
+        hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv);
+        // first digit over all keys, then partition: above -> output group 1, bucket -> candidates
+        hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv);
+        hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv);
+        hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
+                           stv, s.tile_a.p, s.tile_b.p);
+        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv, (int)ST_A,
+                           (int)ST_NC, 0);
+        hipLaunchKernelGGL(k_tk_write, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, (const uint32_t*)nullptr, n,
+                           (const uint64_t*)nullptr, stv, s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p,
+                           (const uint64_t*)nullptr, s.ck.p, s.ci.p, (const uint64_t*)nullptr,
+                           (const uint64_t*)nullptr);
+        // remaining digits on the candidates (device-side count; passes after DONE exit at once)
+        const uint64_t* nc = stv + ST_NC;
+        for (int pass = 0; pass < SEL_PASSES_C; pass++) {
+            hipLaunchKernelGGL(k_tk_hist, dim3(std::min(hg, 512u)), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv);
+            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv);
+        }
+        // candidates above T -> group 2, the first NEED ties -> group 3
+        hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p,
+                           s.tile_b.p);
+        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv, (int)ST_G2,
+                           (int)ST_E2, 1);
+        hipLaunchKernelGGL(k_tk_write, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
+                           s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
+                           stv + ST_NEED);
     } else {
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m);
     }
-    // constant-digit detection
-    hipLaunchKernelGGL(k_sort_ghist, dim3(grid_for(m, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, s.k0.p, m, stv);
-    uint32_t* dflags = (uint32_t*)(stv + 3);   // reuse: word 3 (done flag) no longer needed -> 8 u32 in [3..6]
-    hipLaunchKernelGGL(k_sort_flags, dim3(1), dim3(64), 0, st, stv, m, dflags);
-    SB_HIP(hipMemcpyAsync(s.h_flags, dflags, 32, hipMemcpyDeviceToHost, st));
-    SB_HIP(hipStreamSynchronize(st));
-    int64_t ntiles = (m + TK_TILE - 1) / TK_TILE;
+    hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
+    const int64_t ntiles = (m + TK_TILE - 1) / TK_TILE;
     s.tile_hist.ensure((size_t)ntiles * 256);
-    uint64_t *ka = s.k0.p, *kb = s.k1.p;
-    uint32_t *va = s.v0.p, *vb = s.v1.p;
     for (int p = 0; p < 8; p++) {
-        if (s.h_flags[p]) continue;
-        hipLaunchKernelGGL(k_sort_hist, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, ka, m, 8 * p, s.tile_hist.p, ntiles);
-        scan_exclusive_u32(s.tile_hist.p, s.tile_hist.p, ntiles * 256, nullptr, s.scan, st);
-        hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, ka, va, kb, vb, m, 8 * p,
+        hipLaunchKernelGGL(k_sort_hist, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.k0.p, s.k1.p, m, p, stv,
                            s.tile_hist.p, ntiles);
-        uint64_t* tk = ka; ka = kb; kb = tk;
-        uint32_t* tv = va; va = vb; vb = tv;
+        scan_exclusive_u32(s.tile_hist.p, s.tile_hist.p, ntiles * 256, nullptr, s.scan, st);
+        hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p,
+                           m, p, stv, s.tile_hist.p, ntiles);
     }
-    hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, va, out_idx, m);
+    hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m);
     SB_HIP(hipGetLastError());
     return m;
 }

@@ -109,6 +109,25 @@ def test_device_topk_stable():
         assert np.array_equal(got, exp.astype(np.uint32)), (n, keep, distinct)
 
 
+def test_device_topk_key_ranges():
+    """Select/sort over u64 keys spanning the full range, all-equal keys, keys differing only in low
+    bits, keep > n, and a threshold inside a heavily tied bucket (stable descending order)."""
+    rng = np.random.default_rng(9)
+    cases = [
+        rng.integers(0, 2**64 - 1, 300_000, dtype=np.uint64, endpoint=True),                 # full range
+        np.full(50_000, 12345, dtype=np.uint64),                                               # all equal
+        (np.uint64(0x4010_0000_0000_0000) + rng.integers(0, 4, 200_000).astype(np.uint64)),  # low bits
+        np.repeat(rng.integers(0, 2**63, 7).astype(np.uint64), 30_000),                         # 7 values
+        rng.choice(np.array([0, 1, 2**63, 2**64 - 1], dtype=np.uint64), 100_000),              # extremes
+    ]
+    for keys in cases:
+        n = len(keys)
+        for keep in (1, n // 3, n - 1, n, n + 5):
+            exp = np.lexsort((np.arange(n), ~keys))[:min(keep, n)]
+            got = device_topk(keys, keep)
+            assert np.array_equal(got, exp.astype(np.uint32)), (n, keep, keys[:3])
+
+
 # ---------------------------------------------------------------- whole solves
 def _run_pair(goal, heur, width, seed, use_heuristic=True):
     from splendor_amd.engine import HEURISTIC_IDS
