@@ -88,8 +88,14 @@ int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const dou
 int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_lo, uint64_t root_hi,
               sb_engine** out);
 
-/* One iteration of the `while queue:` loop (src/solver.py:434-457). */
+/* One iteration of the `while queue:` loop (src/solver.py:434-457).  The next turn's expansion is
+ * launched before returning (it overlaps the caller's work); the stats' device times are filled by
+ * sb_turn_times once a turn has completed. */
 int sb_step(sb_engine* e, sb_step_stats* out);
+
+/* Device phase times (ms) of a completed turn, timing flag set (flags bit 0): expand, count+scan,
+ * host gap, emit, top-k, gather, total.  Speedrun handles only; the last 64 turns are kept. */
+int sb_turn_times(sb_engine* e, int32_t turn, float* out7);
 
 /* Number of turns stored (turn 0 = root) and the size of one turn's queue. */
 int sb_num_turns(sb_engine* e, int32_t* out);

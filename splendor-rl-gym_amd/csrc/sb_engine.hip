@@ -21,6 +21,8 @@
 // Visited set: open addressing over 16-byte entries {key, tag}; key = EMPTY marks a free slot.
 // The tag is (turn+1) << 40 | parent rank << 8 | ordinal; tag prefix 0 is the root's turn.
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -465,8 +467,14 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
                                                 uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
                                                 uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
                                                 uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
-                                                uint32_t* __restrict__ err) {
+                                                uint32_t* __restrict__ err, unsigned long long* __restrict__ krange) {
     __shared__ EmShared S;
+    __shared__ unsigned long long kmin, kmax;   // key range for the top-k (sb_sort.hip), one atomic pair per block
+    if (threadIdx.x == 0) {
+        kmin = ~0ull;
+        kmax = 0;
+    }
+    uint64_t tmin = ~0ull, tmax = 0;
     load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = lanemask_lt();
@@ -564,7 +572,7 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
                 const uint32_t cw = S.card[dsc];
                 chi = buy_child_hi(cw, dsc, d, hi, &clo);
                 B += 1;
-                U += d.b[card_color(cw)] == 0;
+                U += ((S.pbon[s] >> (5 * card_color(cw))) & 31) == 0;   // (no dynamic index into d.b)
             } else {
                 chi = st_with_gems(hi, (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]));
             }
@@ -577,10 +585,22 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
 #pragma unroll
                 for (int c = 0; c < NCOL; c++) G += st_gem(chi, c);
                 const double sc = score_vals<H>(T->pw, st_pts(chi), st_saved(chi), G, B, U, T->noise[nv - 1]);
-                skey[kk] = (uint64_t)__double_as_longlong(sc);
+                const uint64_t key = (uint64_t)__double_as_longlong(sc);
+                skey[kk] = key;
+                tmin = key < tmin ? key : tmin;
+                tmax = key > tmax ? key : tmax;
             }
         }
         __syncthreads();
+    }
+    if constexpr (H >= 0) {
+        atomicMin(&kmin, (unsigned long long)tmin);
+        atomicMax(&kmax, (unsigned long long)tmax);
+        __syncthreads();
+        if (threadIdx.x == 0 && kmax >= kmin) {
+            atomicMin(&krange[0], kmin);
+            atomicMax(&krange[1], kmax);
+        }
     }
 }
 
@@ -801,6 +821,8 @@ struct Engine {
     int64_t winner_rank = -1;
     int max_pts = 0;
     uint64_t last_nu = 0;
+    int front_turn = -1;                    // turn whose front half (expand .. readback) is in flight
+    std::vector<hipEvent_t> tev;            // per-turn timing events (TEV_RING x 7)
     Arena turn_mem;
     hipEvent_t ev[8] = {};
     // distributed mode (world_size > 1): owner shard of the global visited set + exchange staging
@@ -827,18 +849,74 @@ static void check_err_word(Engine& E) {
     if (e & 2u) throw HipError{hipErrorInvalidValue, "saved >= 256 exceeds the pow tables"};
 }
 
-static void read_first_table(Engine& E, const Turn& tr) {
-    // the first-rank table for the current beam was written into d_small[8..264) by gather
-    SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 264 * 4, hipMemcpyDeviceToHost, E.s));
-    SB_HIP(hipStreamSynchronize(E.s));
-    check_err_word(E);
-    (void)tr;
-}
-
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
     return ms;
+}
+
+// Step buffers sized up front for a saturated beam (about 12.5 unique children per parent at most on
+// the goal-15 trajectories; DBuf grows past that if ever needed): a hipMalloc/hipFree on the step
+// path would serialise against in-flight work.
+static void preallocate(Engine& E) {
+    const size_t W = (size_t)E.cfg.beam_width, nu = W * 14;
+    E.cand.ensure(W * 3);
+    E.lost.ensure(W * 3);
+    E.cnt.ensure(W);
+    E.off.ensure(W);
+    E.nlo.ensure(nu);
+    E.nhi.ensure(nu);
+    E.npar.ensure(nu);
+    E.skey.ensure(nu);
+    E.kidx.ensure(W);
+    topk_reserve(E.topk, (int64_t)nu, (int64_t)W);
+    E.scan.tiles.ensure(W / SCAN_TILE + 1);
+    E.turn_mem.block_bytes = std::max(E.turn_mem.block_bytes, W * 20 * 8);   // eight beams per block
+}
+
+// Per-turn device timing (flags bit 0): event set [turn % TEV_RING]: 0 expand start, 1 expand end,
+// 2 count+scan end, 3 emit start, 4 emit end, 5 top-k end, 6 gather end.
+constexpr int TEV_RING = 64;
+
+static hipEvent_t* tev(Engine& E, int turn) {
+    if (E.tev.empty()) {
+        E.tev.resize((size_t)TEV_RING * 7);
+        for (auto& ev : E.tev) SB_HIP(hipEventCreate(&ev));
+    }
+    return &E.tev[(size_t)(turn % TEV_RING) * 7];
+}
+
+// Front half of a step for the current beam, launched as soon as that beam exists (right after the
+// previous gather): expansion + claims, survivor counts and offsets, then one readback of the
+// small state: n_unique, error word, the beam's per-pts first-rank table (gather) and n_raw.  The
+// next sb_step waits on this readback only — the goal check and the sizes come from one round trip.
+static void launch_front(Engine& E) {
+    const bool timing = E.cfg.flags & 1;
+    Turn& cur = E.turns.back();
+    const int64_t n = cur.n;
+    hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
+    E.cand.ensure((size_t)n * 3);
+    E.lost.ensure((size_t)n * 3);
+    E.cnt.ensure((size_t)n);
+    E.off.ensure((size_t)n);
+    SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
+    SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
+    const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
+    if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
+    if (n > 0)
+        hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
+                           cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr, E.cand.p,
+                           E.lost.p, E.d_nraw, E.d_small + 1);
+    if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
+    if (n > 0)
+        hipLaunchKernelGGL(k_count_lm, dim3(grid_cap(n, 256, 1u << 14)), dim3(256), 0, E.s, n, E.cand.p, E.lost.p,
+                           E.cnt.p);
+    scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
+    if (timing) SB_HIP(hipEventRecord(ev[2], E.s));
+    SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 264 * 4, hipMemcpyDeviceToHost, E.s));
+    SB_HIP(hipMemcpyAsync(E.h_nraw, E.d_nraw, 8, hipMemcpyDeviceToHost, E.s));
+    SB_HIP(hipGetLastError());
+    E.front_turn = E.turn;
 }
 
 static void engine_step(Engine& E, sb_step_stats* out) {
@@ -853,8 +931,14 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     Turn& cur = E.turns.back();
     const int64_t n = cur.n;
     out->n_parents = n;
+    if (E.front_turn != E.turn) launch_front(E);
+    static const bool htrace = getenv("SB_HOST_TRACE") != nullptr;
+    auto hnow = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double h0 = hnow();
+    SB_HIP(hipStreamSynchronize(E.s));
+    const double h1 = hnow();
+    E.front_turn = -1;
     // ---- goal check and max_pts records, in queue order (src/solver.py:438-445)
-    read_first_table(E, cur);
     const uint32_t* first = E.h_small + 8;
     {
         int64_t win = -1;
@@ -879,7 +963,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
             }
             last_rank = best;
         }
-        if (win >= 0) {
+        if (win >= 0) {   // the speculative front half of this turn is discarded
             E.done = true;
             E.winner_rank = win;
             out->done = 1;
@@ -888,31 +972,8 @@ static void engine_step(Engine& E, sb_step_stats* out) {
             return;
         }
     }
-    const bool heur = E.cfg.use_heuristic != 0;
-    // speculative noise for this step (side stream, overlaps expansion)
-    // keep about two steps of accepted draws ahead of the consumer
-    if (heur && E.noise.produced - E.noise.consumed < std::max<uint64_t>((uint64_t)n * 12, 2 * E.last_nu + (uint64_t)n))
-        noise_generate_async(E.noise, E.s_mt);
-
-    if (timing) SB_HIP(hipEventRecord(E.ev[0], E.s));
-    E.cand.ensure((size_t)n * 3);
-    E.lost.ensure((size_t)n * 3);
-    E.cnt.ensure((size_t)n);
-    E.off.ensure((size_t)n);
-    SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
-    SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
-    const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
-    hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
-                       cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr, E.cand.p,
-                       E.lost.p, E.d_nraw, E.d_small + 1);
-    if (timing) SB_HIP(hipEventRecord(E.ev[1], E.s));
-    hipLaunchKernelGGL(k_count_lm, dim3(grid_cap(n, 256, 1u << 14)), dim3(256), 0, E.s, n, E.cand.p, E.lost.p, E.cnt.p);
-    scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
-    if (timing) SB_HIP(hipEventRecord(E.ev[2], E.s));
-    SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 8, hipMemcpyDeviceToHost, E.s));
-    SB_HIP(hipMemcpyAsync(E.h_nraw, E.d_nraw, 8, hipMemcpyDeviceToHost, E.s));
-    SB_HIP(hipStreamSynchronize(E.s));
     check_err_word(E);
+    const bool heur = E.cfg.use_heuristic != 0;
     const int64_t nu = E.h_small[0];
     out->n_raw = (int64_t)*E.h_nraw;
     out->n_unique = nu;
@@ -937,19 +998,22 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         out->ms_sort = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
         E.last_nu = (uint64_t)nu;
     }
-    if (timing) SB_HIP(hipEventRecord(E.ev[3], E.s));
+    hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
+    if (timing) SB_HIP(hipEventRecord(ev[3], E.s));
+    const double h2 = hnow();
     const unsigned eg = grid_cap(n, EM_PAR, 1u << 15);
     const uint64_t rbase = E.noise.consumed;
     if (!heur) {
         hipLaunchKernelGGL(k_emit_q<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,
                            E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask,
-                           rbase, 0u, E.d_small + 1);
+                           rbase, 0u, E.d_small + 1, (unsigned long long*)nullptr);
     } else {
+        unsigned long long* krange = topk_range_reset(E.topk, E.s);
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
     hipLaunchKernelGGL(k_emit_q<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,        \
                        E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
-                       rbase, 0u, E.d_small + 1);                                                                 \
+                       rbase, 0u, E.d_small + 1, krange);                                                         \
     break;
             case 1: EMIT(1)
             case 2: EMIT(2)
@@ -959,16 +1023,16 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         }
         E.noise.consumed += (uint64_t)nu;
     }
-    if (timing) SB_HIP(hipEventRecord(E.ev[4], E.s));
+    if (timing) SB_HIP(hipEventRecord(ev[4], E.s));
     // ---- prune + next beam
     int64_t m = nu;
     uint32_t* idx = nullptr;
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
-        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s);
+        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true);
         idx = E.kidx.p;
     }
-    if (timing) SB_HIP(hipEventRecord(E.ev[5], E.s));
+    if (timing) SB_HIP(hipEventRecord(ev[5], E.s));
     Turn nt;
     nt.lo = (uint64_t*)E.turn_mem.alloc(m * 8);
     nt.hi = (uint64_t*)E.turn_mem.alloc(m * 8);
@@ -977,22 +1041,36 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
     hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
                        nt.lo, nt.hi, nt.par, E.d_small + 8);
-    if (timing) SB_HIP(hipEventRecord(E.ev[6], E.s));
+    if (timing) SB_HIP(hipEventRecord(ev[6], E.s));
     SB_HIP(hipGetLastError());
     E.turns.push_back(nt);
     E.turn++;
     out->n_kept = m;
     out->noise_draws = E.noise.consumed;
-    if (timing) {
-        SB_HIP(hipEventSynchronize(E.ev[6]));
-        out->ms_expand = ev_ms(E.ev[0], E.ev[1]);
-        out->ms_survive = ev_ms(E.ev[1], E.ev[2]);
-        out->ms_emit = ev_ms(E.ev[3], E.ev[4]);
-        out->ms_select = ev_ms(E.ev[4], E.ev[5]);
-        out->ms_gather = ev_ms(E.ev[5], E.ev[6]);
-        out->ms_mt = ev_ms(E.ev[2], E.ev[3]);   // host round trip for n_unique + any wait on the noise stream
-        out->ms_total = ev_ms(E.ev[0], E.ev[6]);
-    }
+    const double h3 = hnow();
+    launch_front(E);   // the next turn's expansion follows the gather on the stream
+    const double h4 = hnow();
+    if (htrace) fprintf(stderr, "turn %d sync %.3f pre-emit %.3f back %.3f front %.3f\n", E.turn, h1 - h0, h2 - h1, h3 - h2, h4 - h3);
+    // noise for the next turns on the side stream, overlapping that (latency-bound) expansion:
+    // keep about three steps of accepted draws ahead
+    if (heur && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n)
+        noise_generate_async(E.noise, E.s_mt);
+}
+
+// device phase times of a completed turn (timing flag): expand, count+scan, host gap, emit, top-k,
+// gather, total
+static void turn_times(Engine& E, int turn, float* out7) {
+    if (E.tev.empty() || turn < 0 || turn >= E.turn || E.turn - turn > TEV_RING)
+        throw HipError{hipErrorInvalidValue, "no timing for that turn (timing flag off or too old)"};
+    hipEvent_t* ev = tev(E, turn);
+    SB_HIP(hipEventSynchronize(ev[6]));
+    out7[0] = ev_ms(ev[0], ev[1]);
+    out7[1] = ev_ms(ev[1], ev[2]);
+    out7[2] = ev_ms(ev[2], ev[3]);
+    out7[3] = ev_ms(ev[3], ev[4]);
+    out7[4] = ev_ms(ev[4], ev[5]);
+    out7[5] = ev_ms(ev[5], ev[6]);
+    out7[6] = ev_ms(ev[0], ev[6]);
 }
 
 }  // namespace sb
@@ -1141,6 +1219,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
                ring < (1ull << 35))
             ring <<= 1;
         noise_init(E.noise, mt_state625, ring, twists, E.s);
+        if (!distm && cfg->use_heuristic && cfg->beam_width <= (1ll << 24)) preallocate(E);
         SB_HIP(hipStreamSynchronize(E.s));
         return SB_OK;
     });
@@ -1164,6 +1243,15 @@ int sb_step(sb_engine* h, sb_step_stats* out) {
     return guarded([&]() {
         SB_HIP(hipSetDevice(h->E.dev));
         engine_step(h->E, out);
+        return SB_OK;
+    });
+}
+
+int sb_turn_times(sb_engine* h, int32_t turn, float* out7) {
+    if (!h || !out7 || h->E.mode != 0) return SB_ERR_ARG;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(h->E.dev));
+        turn_times(h->E, turn, out7);
         return SB_OK;
     });
 }
@@ -1303,6 +1391,8 @@ void sb_destroy(sb_engine* h) {
     if (E.h_small) (void)hipHostFree(E.h_small);
     if (E.h_nraw) (void)hipHostFree(E.h_nraw);
     for (auto& e : E.ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : E.tev)
         if (e) (void)hipEventDestroy(e);
     if (E.s) (void)hipStreamDestroy(E.s);
     if (E.s_mt) (void)hipStreamDestroy(E.s_mt);

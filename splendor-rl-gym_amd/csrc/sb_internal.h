@@ -96,8 +96,13 @@ struct TopkScratch {
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.
 // Returns the number written (min(n, keep)).  ms_select/ms_sort get device times if non-null.
+// range_ready: the producer of the keys already folded their min/max into the pair returned by
+// topk_range_reset (called before it ran on the same stream).
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st);
+                         hipStream_t st, bool range_ready = false);
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st);
+// size the scratch for n keys and keep kept (avoids allocation on the step path)
+void topk_reserve(TopkScratch& s, int64_t n, int64_t keep);
 
 // ---- MT19937 noise stream (sb_mt.hip) ----
 struct HostMT {

@@ -139,14 +139,18 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
 }
 
 // copy each producer's accepted values to the ring at produced + exclusive offset
+// grid (P, MT_PLACE_SPLIT): block (b, y) copies slice y of producer b's segment
+constexpr int MT_PLACE_SPLIT = 32;
 __global__ __launch_bounds__(256) void k_mt_place(const uint8_t* __restrict__ stage, int64_t seg,
                                                   const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offs,
                                                   uint8_t* __restrict__ ring, uint64_t ring_mask, uint64_t produced) {
     const int64_t b = blockIdx.x;
     const uint32_t n = counts[b];
+    const uint32_t per = (n + MT_PLACE_SPLIT - 1) / MT_PLACE_SPLIT;
+    const uint32_t j0 = blockIdx.y * per, j1 = j0 + per < n ? j0 + per : n;
     const uint64_t base = produced + offs[b];
     const uint8_t* src = stage + b * seg;
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) ring[(base + j) & ring_mask] = src[j];
+    for (uint32_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) ring[(base + j) & ring_mask] = src[j];
 }
 
 constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
@@ -293,7 +297,7 @@ void noise_generate_async(NoiseStream& ns, hipStream_t st) {
     ns.prod.gen_chunk_accepted(ns.stage.p, counts, st);
     SB_HIP(hipMemcpyAsync(offs, counts, (size_t)P * 4, hipMemcpyDeviceToDevice, st));
     scan_tiles_inplace(offs, P, ns.d_total, st);
-    hipLaunchKernelGGL(k_mt_place, dim3(P), dim3(256), 0, st, ns.stage.p, (int64_t)ns.prod.twists * 624, counts, offs,
+    hipLaunchKernelGGL(k_mt_place, dim3(P, MT_PLACE_SPLIT), dim3(256), 0, st, ns.stage.p, (int64_t)ns.prod.twists * 624, counts, offs,
                        ns.ring.p, ns.ring_mask, ns.produced);
     SB_HIP(hipMemcpyAsync(ns.h_total, ns.d_total, 4, hipMemcpyDeviceToHost, st));
     SB_HIP(hipEventRecord(ns.ev_ready, st));

@@ -44,12 +44,12 @@ enum : int {
 
 __device__ __forceinline__ uint64_t hi_bits(uint64_t k, uint64_t sh) { return sh >= 64 ? 0ull : k >> sh; }
 
-__global__ void k_tk_init(uint64_t* st, int64_t keep) {
+__global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range) {
     const int t = threadIdx.x;
-    if (t < ST_HIST) st[t] = 0;
+    if (t < ST_HIST && (t > ST_MAX || !keep_range)) st[t] = 0;
     __syncthreads();
     if (t == 0) {
-        st[ST_MIN] = ~0ull;
+        if (!keep_range) st[ST_MIN] = ~0ull;
         st[ST_NEED] = (uint64_t)keep;
     }
     for (int i = t; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
@@ -361,8 +361,34 @@ void TopkScratch::release() {
     scan.tiles.release();
 }
 
+__global__ void k_tk_range_reset(uint64_t* st) {
+    st[ST_MIN] = ~0ull;
+    st[ST_MAX] = 0;
+}
+
+void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
+    const int64_t m = n < keep ? n : keep;
+    s.k0.ensure(m);
+    s.k1.ensure(m);
+    s.v0.ensure(m);
+    s.v1.ensure(m);
+    s.ck.ensure(n);
+    s.ci.ensure(n);
+    s.tile_a.ensure(n / TK_TILE + 1);
+    s.tile_b.ensure(n / TK_TILE + 1);
+    s.tile_hist.ensure((size_t)(m / TK_TILE + 1) * 256);
+    s.small.ensure(ST_WORDS);
+    s.scan.tiles.ensure((size_t)((m / TK_TILE + 1) * 256) / 4096 + 1);
+}
+
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st) {
+    s.small.ensure(ST_WORDS);
+    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(1), 0, st, s.small.p);
+    return (unsigned long long*)(s.small.p + ST_MIN);
+}
+
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st) {
+                         hipStream_t st, bool range_ready) {
     if (n <= 0 || keep <= 0) return 0;
     const int64_t m = n < keep ? n : keep;
     s.k0.ensure(m);
@@ -371,8 +397,9 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.v1.ensure(m);
     s.small.ensure(ST_WORDS);
     uint64_t* stv = s.small.p;
-    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m);
-    hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
+    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m, (int)range_ready);
+    if (!range_ready)
+        hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
     const bool selected = n > keep;
     if (selected) {
         const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;

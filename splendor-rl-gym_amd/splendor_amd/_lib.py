@@ -27,7 +27,7 @@ SB_ERR_NOTABLES = -5
 # exponents of the host-captured pow tables, in SB row order (include/splendor_beam.h)
 POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
-EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
+EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_turn_times', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
             'sb_get_mt_state', 'sb_sync', 'sb_visited_size', 'sb_destroy', 'sb_last_error', 'sb_version',
             'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk',
             'sbd_goal_table', 'sbd_expand', 'sbd_pack', 'sbd_owner_claim', 'sbd_apply', 'sbd_emit', 'sbd_hist',
@@ -101,6 +101,7 @@ def lib():
         L.sb_init_tables.argtypes = [i32p, f64p, f64p]
         L.sb_create.argtypes = [C.POINTER(SbConfig), u32p, C.c_uint64, C.c_uint64, C.POINTER(vp)]
         L.sb_step.argtypes = [vp, C.POINTER(SbStepStats)]
+        L.sb_turn_times.argtypes = [vp, C.c_int32, np.ctypeslib.ndpointer(np.float32, flags='C')]
         L.sb_num_turns.argtypes = [vp, C.POINTER(C.c_int32)]
         L.sb_turn_size.argtypes = [vp, C.c_int32, C.POINTER(C.c_int64)]
         L.sb_read_turn.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, vp, vp, vp, vp]

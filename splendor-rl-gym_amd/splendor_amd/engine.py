@@ -54,6 +54,13 @@ class BeamEngine:
             self.turn += 1
         return d
 
+    def turn_times(self, t: int) -> dict:
+        """Device phase times (ms) of completed turn t (engine created with timing=True)."""
+        out = np.zeros(7, np.float32)
+        L.check(L.lib().sb_turn_times(self._h, int(t), out), 'sb_turn_times')
+        return dict(zip(('ms_expand', 'ms_survive', 'ms_mt', 'ms_emit', 'ms_select', 'ms_gather', 'ms_total'),
+                        (float(x) for x in out)))
+
     def num_turns(self) -> int:
         n = C.c_int32()
         L.check(L.lib().sb_num_turns(self._h, C.byref(n)))
