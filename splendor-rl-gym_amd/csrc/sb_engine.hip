@@ -143,8 +143,27 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
 }
 
 // ------------------------------------------------------------------ k_expand
-constexpr int XP_NT = 256;            // 4 waves
-constexpr int XP_PAR = 16;            // parents per block iteration (4 per wave)
+// tuning knobs (overridable with -D for experiments; see profiles/variants.sh)
+#ifndef SB_XP_PAR
+#define SB_XP_PAR 32
+#endif
+#ifndef SB_XP_WAVES
+#define SB_XP_WAVES 1
+#endif
+#ifndef SB_EM_PAR
+#define SB_EM_PAR 32
+#endif
+#ifndef SB_XP_NT
+#define SB_XP_NT 256
+#endif
+#ifndef SB_WAVE_EXPAND
+#define SB_WAVE_EXPAND 0   // 1: wave-autonomous expansion (sb_wave.inc); 0: workgroup-queue form
+#endif
+#ifndef SB_WAVE_EMIT
+#define SB_WAVE_EMIT 1     // 1: wave-autonomous emission (sb_wave.inc); 0: workgroup-queue form
+#endif
+constexpr int XP_NT = SB_XP_NT;       // 4 waves
+constexpr int XP_PAR = SB_XP_PAR;     // parents per block iteration (<= 32)
 
 struct XpShared {
     uint32_t card[NCARDS];
@@ -208,7 +227,7 @@ __device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* 
 // LM (lost marking): displaced same-turn claims are marked in `lost`; otherwise (sharded path) each
 // raw child's desc byte and visited slot are written at [rank*MAX_CHILDREN + ordinal].
 template <bool LM>
-__global__ __launch_bounds__(XP_NT) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
+__global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
                                                   uint64_t mask, uint64_t turn_tag, uint8_t* __restrict__ desc,
                                                   uint32_t* __restrict__ rslot, unsigned long long* __restrict__ cand,
@@ -438,7 +457,7 @@ __device__ __forceinline__ bool mask_bit(uint64_t m0, uint64_t m1, uint64_t m2, 
 // Phase A: a wave per parent re-enumerates its children in canonical order and queues the survivors
 // (cand & ~lost) with their rank inside the parent.  Phase B: all threads build the queued children
 // densely — state, parent link, float64 score with the MT noise of its next_queue position.
-constexpr int EM_PAR = 32;
+constexpr int EM_PAR = SB_EM_PAR;   // <= 32
 struct EmShared {
     uint32_t card[NCARDS];
     int32_t pdelta[4][NPAT_MAX];
@@ -603,6 +622,8 @@ __global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, co
         }
     }
 }
+
+#include "sb_wave.inc"
 
 // ------------------------------------------------------------------ beam write + per-pts first rank
 __global__ __launch_bounds__(256) void k_gather(const uint32_t* __restrict__ idx, int64_t m,
@@ -872,6 +893,7 @@ static void preallocate(Engine& E) {
     topk_reserve(E.topk, (int64_t)nu, (int64_t)W);
     E.scan.tiles.ensure(W / SCAN_TILE + 1);
     E.turn_mem.block_bytes = std::max(E.turn_mem.block_bytes, W * 20 * 8);   // eight beams per block
+    E.turn_mem.reserve(W * 20 * 24);   // a goal-15 run keeps < 24 saturated beams: no hipMalloc mid-run
 }
 
 // Per-turn device timing (flags bit 0): event set [turn % TEV_RING]: 0 expand start, 1 expand end,
@@ -903,10 +925,15 @@ static void launch_front(Engine& E) {
     SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
     if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
-    if (n > 0)
-        hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
-                           cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr, E.cand.p,
-                           E.lost.p, E.d_nraw, E.d_small + 1);
+    if (n > 0) {
+        if (SB_WAVE_EXPAND)
+            hipLaunchKernelGGL(k_expand_w, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi,
+                               n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
+        else
+            hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables,
+                               cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr,
+                               E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
+    }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)
         hipLaunchKernelGGL(k_count_lm, dim3(grid_cap(n, 256, 1u << 14)), dim3(256), 0, E.s, n, E.cand.p, E.lost.p,
@@ -1001,17 +1028,18 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
     if (timing) SB_HIP(hipEventRecord(ev[3], E.s));
     const double h2 = hnow();
-    const unsigned eg = grid_cap(n, EM_PAR, 1u << 15);
+    const unsigned eg = SB_WAVE_EMIT ? grid_cap(n, 256, 8192) : grid_cap(n, EM_PAR, 1u << 15);
     const uint64_t rbase = E.noise.consumed;
+#define EMIT_K(H) (SB_WAVE_EMIT ? k_emit_w<H> : k_emit_q<H>)
     if (!heur) {
-        hipLaunchKernelGGL(k_emit_q<-1>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,
-                           E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask,
-                           rbase, 0u, E.d_small + 1, (unsigned long long*)nullptr);
+        hipLaunchKernelGGL(EMIT_K(-1), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, E.lost.p,
+                           E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase, 0u,
+                           E.d_small + 1, (unsigned long long*)nullptr);
     } else {
         unsigned long long* krange = topk_range_reset(E.topk, E.s);
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
-    hipLaunchKernelGGL(k_emit_q<H>, dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,        \
+    hipLaunchKernelGGL(EMIT_K(H), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,          \
                        E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
                        rbase, 0u, E.d_small + 1, krange);                                                         \
     break;
@@ -1021,6 +1049,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
             default: EMIT(0)
 #undef EMIT
         }
+#undef EMIT_K
         E.noise.consumed += (uint64_t)nu;
     }
     if (timing) SB_HIP(hipEventRecord(ev[4], E.s));

@@ -48,6 +48,15 @@ struct Arena {
     char* cur = nullptr;
     size_t left = 0;
     size_t block_bytes = (size_t)256 << 20;
+    void reserve(size_t bytes) {   // make sure the next `bytes` come from one block already allocated
+        if (bytes <= left) return;
+        const size_t b = bytes > block_bytes ? bytes : block_bytes;
+        void* p = nullptr;
+        SB_HIP(hipMalloc(&p, b));
+        blocks.push_back(p);
+        cur = (char*)p;
+        left = b;
+    }
     void* alloc(size_t bytes) {
         bytes = (bytes + 255) & ~(size_t)255;
         if (bytes > left) {

@@ -15,6 +15,8 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(PKG_DIR), 'csrc')
 LIB_PATH = os.path.join(PKG_DIR, 'libsplendor_beam.so')
+# developer knob: load a differently tuned build of the same sources (profiles/variants.sh)
+LOAD_PATH = os.environ.get('SPLENDOR_BEAM_LIB', LIB_PATH)
 SOURCES = ['sb_engine.hip', 'sb_scan.hip', 'sb_sort.hip', 'sb_mt.hip', 'sb_gf2.hip']
 
 SB_OK = 0
@@ -62,15 +64,16 @@ class SbStepStats(C.Structure):
         return d
 
 
-def build(verbose: bool = False) -> str:
-    """Compile the HIP sources for gfx950 into the in-tree shared library."""
+def build(verbose: bool = False, out: str | None = None, defines: tuple = ()) -> str:
+    """Compile the HIP sources for gfx950 into the in-tree shared library (or `out`, with -D `defines`)."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    out = out or LIB_PATH
     cmd = ['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',
-           '-Wall', '-Wno-unused-function', *srcs, '-o', LIB_PATH]
+           '-Wall', '-Wno-unused-function', *[f'-D{d}' for d in defines], *srcs, '-o', out]
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True)
-    return LIB_PATH
+    return out
 
 
 def _stale() -> bool:
@@ -90,9 +93,9 @@ def lib():
     """Load (never silently replace) the engine library."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f'{LIB_PATH} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)')
-        L = C.CDLL(LIB_PATH)
+        if not os.path.exists(LOAD_PATH):
+            raise ImportError(f'{LOAD_PATH} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)')
+        L = C.CDLL(LOAD_PATH)
         u64p = np.ctypeslib.ndpointer(np.uint64, flags='C')
         u32p = np.ctypeslib.ndpointer(np.uint32, flags='C')
         i32p = np.ctypeslib.ndpointer(np.int32, flags='C')
