@@ -124,6 +124,58 @@ __device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t
     return true;
 }
 
+// visit_claim_lm with the entry at the key's home slot already loaded (ent)
+__device__ __forceinline__ bool visit_claim_lm_pre(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
+                                                   uint64_t tag, unsigned long long* __restrict__ lost, uint32_t* err) {
+    uint64_t h = mix64(key) & mask;
+    uint64_t cur;
+    for (int probe = 0;; probe++) {
+        if (probe > 0) ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);
+        uint64_t k = ent.x;
+        if (k == EMPTY) {
+            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
+                                      (unsigned long long)key);
+            if (prev == EMPTY) {
+                cur = EMPTY;
+                break;
+            }
+            if (prev == key) {
+                cur = tab[h].tag;
+                break;
+            }
+            k = prev;
+        }
+        if (k == key) {
+            cur = ent.y;
+            break;
+        }
+        h = (h + 1) & mask;
+        if (probe >= MAX_PROBE) {
+            atomicOr(err, 1u);
+            return false;
+        }
+    }
+#ifdef SB_CLAIM_STATS
+    // err[1] old-turn keys, err[2] inserted, err[3] same-turn early-out, err[4] lost at atomicMin, err[5] displaced
+    if (cur != EMPTY && cur < (tag & ~((1ull << 40) - 1))) atomicAdd(err + 1, 1u);
+    else if (cur == EMPTY) atomicAdd(err + 2, 1u);
+    else if (cur < tag) atomicAdd(err + 3, 1u);
+#endif
+    if (cur != EMPTY && cur < tag) return false;
+    const uint64_t old = atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+#ifdef SB_CLAIM_STATS
+    if (old < tag) atomicAdd(err + 4, 1u);
+    else if (old != EMPTY) atomicAdd(err + 5, 1u);
+#endif
+    if (old < tag) return false;
+    if (old != EMPTY) {
+        const uint64_t ro = (old >> 8) & 0xFFFFFFFFull;
+        const uint32_t oo = (uint32_t)(old & 255);
+        atomicOr(&lost[ro * 3 + (oo >> 6)], 1ull << (oo & 63));
+    }
+    return true;
+}
+
 __device__ __forceinline__ uint64_t lookup_tag(const Entry* __restrict__ tab, uint64_t mask, uint64_t key) {
     uint64_t h = mix64(key) & mask;
     for (int probe = 0; probe <= MAX_PROBE; probe++) {
@@ -155,6 +207,14 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
 #endif
 #ifndef SB_XP_NT
 #define SB_XP_NT 256
+#endif
+#ifndef SB_XP_U
+#define SB_XP_U 1          // children per thread per phase-B round (probe loads in flight together)
+#endif
+constexpr int XP_U = SB_XP_U;
+
+#ifndef SB_XP_GRID_CAP
+#define SB_XP_GRID_CAP (1u << 15)
 #endif
 #ifndef SB_WAVE_EXPAND
 #define SB_WAVE_EXPAND 0   // 1: wave-autonomous expansion (sb_wave.inc); 0: workgroup-queue form
@@ -307,34 +367,57 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
         }
         __syncthreads();
-        // ---- phase B: dense child processing: key, visited probe + claim
+        // ---- phase B: dense child processing: key, visited probe + claim.  LM: XP_U children per
+        // thread with their first probe loads issued together (more misses in flight per wave).
         const uint32_t nq = S.nq;
-        for (uint32_t i = t; i < nq; i += XP_NT) {
-            const uint32_t e = S.q[i];
-            const int s = (int)(e & 31), o = (int)((e >> 5) & 255), dsc = (int)(e >> 13);
+        auto child_key = [&](uint32_t e) -> uint64_t {
+            const int s = (int)(e & 31), dsc = (int)(e >> 13);
             const uint64_t lo = S.plo[s], hi = S.phi[s];
-            uint64_t key;
             if (dsc < NCARDS) {
                 Derived d;
                 derive_packed(hi, S.pbon[s], d);
                 uint64_t clo = lo;
                 const uint64_t chi = buy_child_hi(S.card[dsc], dsc, d, hi, &clo);
-                key = state_key(hash_cards(clo, st_chi(chi)), hash_gems(st_gemfield(chi)));
-            } else {
-                const uint32_t gf = (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]);
-                key = state_key(S.phc[s], hash_gems(gf));
+                return state_key(hash_cards(clo, st_chi(chi)), hash_gems(st_gemfield(chi)));
             }
-            const int64_t r = base + s;
-            const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
-            bool c;
-            if constexpr (LM) {
-                c = visit_claim_lm(tab, mask, key, tag, lost, err);
-            } else {
+            const uint32_t gf = (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]);
+            return state_key(S.phc[s], hash_gems(gf));
+        };
+        if constexpr (LM) {
+            for (uint32_t i0 = t; i0 < nq; i0 += XP_NT * XP_U) {
+                uint32_t e[XP_U];
+                uint64_t key[XP_U];
+                ulonglong2 ent[XP_U];
+#pragma unroll
+                for (int u = 0; u < XP_U; u++) {
+                    const uint32_t i = i0 + u * XP_NT;
+                    e[u] = i < nq ? S.q[i] : 0xFFFFFFFFu;
+                    key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < XP_U; u++)
+                    if (e[u] != 0xFFFFFFFFu) ent[u] = *reinterpret_cast<const ulonglong2*>(&tab[mix64(key[u]) & mask]);
+#pragma unroll
+                for (int u = 0; u < XP_U; u++) {
+                    if (e[u] == 0xFFFFFFFFu) continue;
+                    const int s = (int)(e[u] & 31), o = (int)((e[u] >> 5) & 255);
+                    const uint64_t tag = turn_tag | ((uint64_t)(base + s) << 8) | (uint64_t)o;
+                    if (visit_claim_lm_pre(tab, mask, key[u], ent[u], tag, lost, err))
+                        atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
+                }
+            }
+        } else {
+            for (uint32_t i = t; i < nq; i += XP_NT) {
+                const uint32_t e = S.q[i];
+                const int s = (int)(e & 31), o = (int)((e >> 5) & 255);
+                const uint64_t key = child_key(e);
+                const int64_t r = base + s;
+                const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
                 uint32_t slot;
-                c = visit_claim(tab, mask, key, tag, &slot, err);
+                const bool c = visit_claim(tab, mask, key, tag, &slot, err);
                 rslot[r * MAX_CHILDREN + o] = slot;
+                if (c) atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
             }
-            if (c) atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
         }
         __syncthreads();
         if (t < XP_PAR * 3) {
@@ -923,6 +1006,7 @@ static void launch_front(Engine& E) {
     E.off.ensure((size_t)n);
     SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
     SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
+    SB_HIP(hipMemsetAsync(E.d_small + 2, 0, 6 * 4, E.s));   // claim statistics (SB_CLAIM_STATS builds): [2..8)
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
     if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
     if (n > 0) {
@@ -930,7 +1014,9 @@ static void launch_front(Engine& E) {
             hipLaunchKernelGGL(k_expand_w, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi,
                                n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
         else
-            hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, 1u << 15)), dim3(XP_NT), 0, E.s, E.d_tables,
+            // one block per group of parents (no grid-stride): blocks dispatch in rank order, so most
+            // same-turn duplicates arrive smallest tag first and resolve by a plain load
+            hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
                                cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr,
                                E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
     }
@@ -1079,7 +1165,10 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     const double h3 = hnow();
     launch_front(E);   // the next turn's expansion follows the gather on the stream
     const double h4 = hnow();
-    if (htrace) fprintf(stderr, "turn %d sync %.3f pre-emit %.3f back %.3f front %.3f\n", E.turn, h1 - h0, h2 - h1, h3 - h2, h4 - h3);
+    if (htrace)
+        fprintf(stderr, "turn %d sync %.3f pre-emit %.3f back %.3f front %.3f | old %u ins %u dup_early %u dup_lost %u displaced %u\n",
+                E.turn, h1 - h0, h2 - h1, h3 - h2, h4 - h3, E.h_small[2], E.h_small[3], E.h_small[4], E.h_small[5],
+                E.h_small[6]);
     // noise for the next turns on the side stream, overlapping that (latency-bound) expansion:
     // keep about three steps of accepted draws ahead
     if (heur && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n)
