@@ -1014,8 +1014,8 @@ static void launch_front(Engine& E) {
             hipLaunchKernelGGL(k_expand_w, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi,
                                n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
         else
-            // one block per group of parents (no grid-stride): blocks dispatch in rank order, so most
-            // same-turn duplicates arrive smallest tag first and resolve by a plain load
+            // grid-stride over groups of XP_PAR parents (an uncapped one-group-per-block grid measured
+            // slower: same-turn duplicates come from all over the beam, not from nearby ranks)
             hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
                                cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr,
                                E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
