@@ -38,6 +38,9 @@ def parse():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
+    ap.add_argument('--realistic', action='store_true',
+                    help='config C4 instead: realistic 2-player goal 15 --shuffle, W=1M (a separate line, not the '
+                         'headline metric)')
     return ap.parse_args()
 
 
@@ -129,8 +132,52 @@ def run_single(args):
     return per, elapsed, setup_turns
 
 
+def run_realistic(args):
+    """Config C4: MultiPlayerState beam search, 2 players, goal 15, shuffled market (seed 0), W=1M."""
+    from splendor_amd.engine_rt import RealisticEngine
+    from splendor_amd.realistic import GameConfig, MultiPlayerState
+    width = args.width if args.width != 4_000_000 else 1_000_000
+    cfg = GameConfig(num_players=2, target_points=15, gems_per_color=4, infinite_resources=False)
+    root = MultiPlayerState.newgame(config=cfg, shuffle_market=True, seed=args.seed)
+    random.seed(args.seed)
+    eng = RealisticEngine(root, beam_width=width, mt_state625=random.getstate()[1], device=0)
+    setup = 0
+    while True:
+        r = eng.step()
+        setup += 1
+        if r['n_kept'] >= width or r['done']:
+            break
+    for _ in range(args.warmup):
+        eng.step()
+    import ctypes
+    from splendor_amd import _lib
+    _lib.lib().sb_sync(eng._h)
+    per = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        per.append(eng.step())
+        if per[-1]['done']:
+            break
+    _lib.lib().sb_sync(eng._h)
+    elapsed = time.perf_counter() - t0
+    eng.close()
+    parents = sum(p['n_parents'] for p in per)
+    out = {'metric': 'states expanded/sec per beam step, realistic 2-player goal 15 --shuffle, beam_width=1M',
+           'value': round(parents / elapsed, 1), 'unit': 'states/s', 'n_gpus': 1, 'steps': len(per),
+           'warmup': args.warmup, 'ms_per_step': round(elapsed / len(per) * 1e3, 3), 'higher_is_better': True,
+           'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64+f64',
+           'data': f'synthetic: seeded realistic solve trajectory (market shuffle seed {args.seed}, random.seed('
+                   f'{args.seed})), saturated turns {setup + args.warmup}..{setup + args.warmup + len(per) - 1}',
+           'config': {'workload': f'realistic 2p goal_pts=15 --shuffle beam_width={width} (C4)', 'beam_width': width,
+                      'b_raw': round(sum(p['n_raw'] for p in per) / parents, 3),
+                      'b_uniq': round(sum(p['n_unique'] for p in per) / parents, 3)}}
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.realistic:
+        return run_realistic(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1 or args.gpus > 1:
         import bench_dist

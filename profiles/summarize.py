@@ -15,7 +15,9 @@ import os
 import re
 from collections import defaultdict
 
-PER_STEP = ['k_expand', 'k_survive', 'k_emit<', 'k_gather', 'k_sel_write', 'k_sel_count']
+# kernels launched once per step on the saturated path (k_expand: the last launches include the
+# pipelined expansion of the turn after the last timed one — one per step either way)
+PER_STEP = ['k_expand', 'k_count_lm', 'k_emit_w<1>', 'k_tk_count', 'k_tk_write', 'k_gather', 'k_copy_idx']
 
 
 def short(name):
@@ -38,7 +40,7 @@ def main():
         kernels[k] = {'calls': len(durs), 'total_ns': sum(durs), 'avg_ns': sum(durs) / len(durs)}
     # timed-step view of the per-step kernels
     timed = {}
-    for k in ('k_expand', 'k_survive', 'k_emit<1>', 'k_gather'):
+    for k in PER_STEP:
         if k in by:
             d = by[k][-a.steps:]
             timed[k] = {'launches': len(d), 'avg_ns': sum(d) / len(d)}
