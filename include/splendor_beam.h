@@ -154,6 +154,16 @@ int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, const uint64_t* d_tag, 
 int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
 /* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */
 int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
+/* Sharded noise stream (world > 1, heuristic): rank r owns MT19937 chunks c = r (mod world), each
+ * P producer segments of twists*624 words.  sbd_noise_info: [P, twists, accepted values in the lead
+ * block, consumed].  sbd_noise_chunk: the P windows (624 u32 each, device buffer win_out) of the
+ * rank's next owned chunk and its per-producer accepted counts (host).  sbd_noise_fill: regenerate
+ * nseg producer segments (device window addresses, global index of each one's first accepted draw)
+ * and store the accepted values with global index in [a, b) for this rank's emission. */
+int sbd_noise_info(sb_engine* e, uint64_t* out4);
+int sbd_noise_chunk(sb_engine* e, void* win_out, uint32_t* counts_host);
+int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
+
 /* radix-select pass: histogram of the next 8 bits of keys whose top `bits` bits equal pref[j] */
 int sbd_hist(sb_engine* e, int32_t nb, const uint64_t* pref_host, int32_t bits, int64_t* hist_host);
 int sbd_eq_count(sb_engine* e, uint64_t T, int64_t* out);

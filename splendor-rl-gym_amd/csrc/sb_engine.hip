@@ -1337,6 +1337,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
                ring < (1ull << 35))
             ring <<= 1;
         noise_init(E.noise, mt_state625, ring, twists, E.s);
+        if (distm && cfg->use_heuristic) noise_shard_setup(E.noise, cfg->rank, cfg->world_size, E.s);
         if (!distm && cfg->use_heuristic && cfg->beam_width <= (1ll << 24)) preallocate(E);
         SB_HIP(hipStreamSynchronize(E.s));
         return SB_OK;

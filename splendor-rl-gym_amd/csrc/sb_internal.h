@@ -127,6 +127,7 @@ struct MTProducers {
     uint32_t* d_win = nullptr;     // P x 624 segment-start windows
     uint32_t* d_poly = nullptr;    // jump polynomials (doubling tree + chunk stride)
     uint32_t* chunk_poly = nullptr;
+    uint32_t* stride_poly = nullptr;   // sharded: jump world * P * L (to this rank's next chunk)
     void init(const uint32_t origin[624], int P, int64_t twists, hipStream_t st);
     void gen_chunk(uint32_t* out, hipStream_t st);   // P*L tempered words
     void gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st);   // accepted values per producer
@@ -148,6 +149,8 @@ struct NoiseStream {
     ScanScratch scan;
     hipEvent_t ev_ready = nullptr;
     bool pending = false;
+    bool sharded = false;          // world > 1: values come from noise_shard_fill
+    DBuf<uint64_t> segtab;         // sharded fill: segment windows + first accepted indices
 };
 void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, int64_t twists, hipStream_t st);
 uint64_t noise_chunk_words(const NoiseStream& ns);
@@ -157,6 +160,13 @@ void noise_generate_async(NoiseStream& ns, hipStream_t st);
 // Block until the ring holds >= need unconsumed values (generating more if necessary).
 void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st);
 void noise_free(NoiseStream& ns);
+// Sharded stream (world > 1): chunks c = rank (mod world) are this rank's.  setup jumps the producers
+// to chunk `rank`; chunk() copies the P producer windows of the next owned chunk to d_win_out and
+// returns its per-producer accepted counts; fill() regenerates producer segments into the ring.
+void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st);
+void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* h_counts, hipStream_t st);
+void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+                      hipStream_t st);
 void noise_mt_state(NoiseStream& ns, uint32_t* out625);
 // debug: raw device words from P producers of `twists` twists per segment
 void mt_debug_words(const uint32_t* state625, int64_t n, int P, int64_t twists, uint32_t* out);

@@ -15,6 +15,8 @@
 //               values, so next_queue element k reads ring[(consumed + k) & mask].
 #include <string.h>
 
+#include <vector>
+
 #include "sb_block.h"
 #include "sb_gf2.h"
 #include "sb_internal.h"
@@ -88,13 +90,15 @@ __global__ __launch_bounds__(MT_NT) void k_mt_write(const uint32_t* __restrict__
     }
 }
 
-// P producers, one workgroup each; producer b runs `twists` twists from window b.  Raw mode writes
-// the tempered words (debug); compact mode writes only the accepted randint values (1..100) of the
-// segment, in order, to stage[b * L ..] and their count to counts[b] (fused accept compaction).
-template <bool RAW>
+// P producers, one workgroup each; producer b runs `twists` twists from window b.  MODE 0 (raw) writes
+// the tempered words (debug); MODE 1 (compact) writes only the accepted randint values (1..100) of
+// the segment, in order, to stage[b * L ..] and their count to counts[b] (fused accept compaction);
+// MODE 2 (count) only counts them (sharded streams, see noise_shard_chunk).
+template <int MODE>
 __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
                                                      uint8_t* __restrict__ stage, uint32_t* __restrict__ counts,
                                                      int64_t twists) {
+    constexpr bool RAW = MODE == 0;
     __shared__ uint32_t buf[2][624];
     __shared__ uint32_t wc[10];
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
                 before += x < wv ? c : 0u;
                 total += c;
             }
-            if (acc) sg[run + before + __popcll(m & lanemask_lt())] = (uint8_t)((y >> 25) + 1);
+            if (MODE == 1 && acc) sg[run + before + __popcll(m & lanemask_lt())] = (uint8_t)((y >> 25) + 1);
             run += total;
         }
         cur ^= 1;
@@ -151,6 +155,50 @@ __global__ __launch_bounds__(256) void k_mt_place(const uint8_t* __restrict__ st
     const uint64_t base = produced + offs[b];
     const uint8_t* src = stage + b * seg;
     for (uint32_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) ring[(base + j) & ring_mask] = src[j];
+}
+
+// Sharded streams: block j regenerates one producer segment from its window seg_win[j] (device
+// address of 624 words); its first accepted draw has global index seg_acc0[j].  Accepted values
+// with global index in [a, b) go to ring[index & ring_mask]; the block stops once past b.
+__global__ __launch_bounds__(640) void k_mt_fill(const uint64_t* __restrict__ seg_win, const uint64_t* __restrict__ seg_acc0,
+                                                  int64_t twists, uint64_t a, uint64_t b, uint8_t* __restrict__ ring,
+                                                  uint64_t ring_mask) {
+    __shared__ uint32_t buf[2][624];
+    __shared__ uint32_t wc[10];
+    const int t = threadIdx.x, wv = t >> 6;
+    const uint32_t* win = reinterpret_cast<const uint32_t*>(seg_win[blockIdx.x]);
+    if (t < 624) buf[0][t] = win[t];
+    __syncthreads();
+    uint64_t run = seg_acc0[blockIdx.x];
+    int cur = 0;
+    for (int64_t w = 0; w < twists && run < b; w++) {
+        uint32_t* A = buf[cur];
+        uint32_t* B = buf[cur ^ 1];
+        if (t < 227) B[t] = mt_mix(A[t], A[t + 1], A[t + 397]);
+        __syncthreads();
+        if (t < 227) B[227 + t] = mt_mix(A[227 + t], A[228 + t], B[t]);
+        __syncthreads();
+        if (t < 169) B[454 + t] = mt_mix(A[454 + t], A[455 + t], B[227 + t]);
+        else if (t == 169) B[623] = mt_mix(A[623], B[0], B[396]);
+        __syncthreads();
+        const uint32_t y = t < 624 ? mt_temper(B[t]) : 0u;
+        const bool acc = t < 624 && (y >> 25) < 100u;
+        const uint64_t m = __ballot(acc);
+        if ((t & 63) == 0) wc[wv] = __popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int x = 0; x < 10; x++) {
+            const uint32_t c = wc[x];
+            before += x < wv ? c : 0u;
+            total += c;
+        }
+        const uint64_t idx = run + before + __popcll(m & lanemask_lt());
+        if (acc && idx >= a && idx < b) ring[idx & ring_mask] = (uint8_t)((y >> 25) + 1);
+        run += total;
+        cur ^= 1;
+        __syncthreads();   // wc is rewritten by the next twist
+    }
 }
 
 constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
@@ -223,7 +271,7 @@ void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipS
 void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
     if (chunk > 0)   // every producer jumps P*L ahead of its previous segment start
         hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
-    hipLaunchKernelGGL(k_mt_gen_par<true>, dim3(P), dim3(640), 0, st, d_win, out, (uint8_t*)nullptr,
+    hipLaunchKernelGGL(k_mt_gen_par<0>, dim3(P), dim3(640), 0, st, d_win, out, (uint8_t*)nullptr,
                        (uint32_t*)nullptr, twists);
     SB_HIP(hipGetLastError());
     chunk++;
@@ -232,7 +280,7 @@ void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
 void MTProducers::gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st) {
     if (chunk > 0)
         hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
-    hipLaunchKernelGGL(k_mt_gen_par<false>, dim3(P), dim3(640), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
+    hipLaunchKernelGGL(k_mt_gen_par<1>, dim3(P), dim3(640), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
                        twists);
     SB_HIP(hipGetLastError());
     chunk++;
@@ -241,7 +289,8 @@ void MTProducers::gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream
 void MTProducers::release() {
     if (d_win) (void)hipFree(d_win);
     if (d_poly) (void)hipFree(d_poly);
-    d_win = d_poly = nullptr;
+    if (stride_poly) (void)hipFree(stride_poly);
+    d_win = d_poly = stride_poly = nullptr;
 }
 
 static void compact_accepted(NoiseStream& ns, const uint32_t* raw, int64_t n, hipStream_t st) {
@@ -335,11 +384,52 @@ void noise_mt_state(NoiseStream& ns, uint32_t* out625) {
     out625[624] = (uint32_t)ns.replay.idx;
 }
 
+// ---- sharded stream (world > 1): this rank owns chunks c = rank, rank + world, ...
+void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st) {
+    MTProducers& pr = ns.prod;
+    for (int k = 0; k < rank; k++)   // producers to chunk `rank`
+        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.chunk_poly);
+    const uint64_t L = (uint64_t)pr.twists * 624;
+    std::vector<uint32_t> w(624);
+    gf2::to_words(gf2::jump_poly(L * (uint64_t)pr.P * (uint64_t)world), w.data());
+    SB_HIP(hipMalloc((void**)&pr.stride_poly, 624 * 4));
+    SB_HIP(hipMemcpyAsync(pr.stride_poly, w.data(), 624 * 4, hipMemcpyHostToDevice, st));
+    SB_HIP(hipStreamSynchronize(st));
+    pr.chunk = 0;
+    ns.sharded = true;
+}
+
+void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* h_counts, hipStream_t st) {
+    MTProducers& pr = ns.prod;
+    if (pr.chunk > 0)
+        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
+    SB_HIP(hipMemcpyAsync(d_win_out, pr.d_win, (size_t)pr.P * 624 * 4, hipMemcpyDeviceToDevice, st));
+    ns.scan.tiles.ensure((size_t)pr.P);
+    hipLaunchKernelGGL(k_mt_gen_par<2>, dim3(pr.P), dim3(640), 0, st, pr.d_win, (uint32_t*)nullptr, (uint8_t*)nullptr,
+                       ns.scan.tiles.p, pr.twists);
+    SB_HIP(hipMemcpyAsync(h_counts, ns.scan.tiles.p, (size_t)pr.P * 4, hipMemcpyDeviceToHost, st));
+    SB_HIP(hipStreamSynchronize(st));
+    pr.chunk++;
+}
+
+void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+                      hipStream_t st) {
+    if (nseg <= 0 || a >= b) return;
+    ns.segtab.ensure((size_t)nseg * 2);
+    SB_HIP(hipMemcpyAsync(ns.segtab.p, h_win, (size_t)nseg * 8, hipMemcpyHostToDevice, st));
+    SB_HIP(hipMemcpyAsync(ns.segtab.p + nseg, h_acc0, (size_t)nseg * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_mt_fill, dim3(nseg), dim3(640), 0, st, ns.segtab.p, ns.segtab.p + nseg, ns.prod.twists, a, b,
+                       ns.ring.p, ns.ring_mask);
+    SB_HIP(hipGetLastError());
+    SB_HIP(hipStreamSynchronize(st));   // the host table is reused by the caller
+}
+
 void noise_free(NoiseStream& ns) {
     if (ns.d_total) (void)hipFree(ns.d_total);
     if (ns.h_total) (void)hipHostFree(ns.h_total);
     if (ns.ev_ready) (void)hipEventDestroy(ns.ev_ready);
     ns.prod.release();
+    ns.segtab.release();
     ns.raw.release();
     ns.stage.release();
     ns.ring.release();

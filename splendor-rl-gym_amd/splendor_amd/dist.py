@@ -73,6 +73,20 @@ class Comm:
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
+    def allgather_array(self, arr: np.ndarray) -> np.ndarray:
+        """(world, len) int64 array of every rank's equal-length int vector."""
+        t = self._to(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device))
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return np.stack([x.cpu().numpy() for x in out])
+
+    def allgather_tensor(self, t: torch.Tensor) -> list[torch.Tensor]:
+        """Every rank's equal-shape tensor, on this rank's device."""
+        s = self._to(t)
+        out = [torch.empty_like(s) for _ in range(self.world)]
+        dist.all_gather(out, s)
+        return [self._back(x) for x in out]
+
     def broadcast_ints(self, vals, src: int) -> list[int]:
         t = self._to(torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device))
         dist.broadcast(t, src)
@@ -84,6 +98,50 @@ class Comm:
 
 def _u64_to_i64(x: int) -> int:
     return x - (1 << 64) if x >= (1 << 63) else x
+
+
+class ShardNoise:
+    """The randint(1,100) stream without replicated generation.
+
+    The k-th next_queue entry scores with the k-th accepted MT19937 draw (src/solver.py:452-456);
+    rank r emits entries [k_off, k_off + n_loc) of each turn.  The raw stream after the lead block is
+    cut into chunks of P producer segments; rank r generates chunks c = r (mod world) in count-only
+    mode, every rank all-gathers the per-producer accepted counts and start windows, and each rank
+    regenerates just the producer segments that cover its own window.  Per step a rank generates
+    about 2/world of the stream instead of all of it.
+    """
+
+    def __init__(self, backend, comm: Comm):
+        self.b, self.c = backend, comm
+        info = backend.noise_info()
+        self.P = int(info[0])
+        self.gen_total = int(info[2])   # accepted draws available (global index), the lead block first
+        self.chunks = []                # (first global accepted index, cumulative counts (P+1), windows)
+
+    def prepare(self, A: int, N: int, k_off: int, n_loc: int):
+        """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission."""
+        c, b = self.c, self.b
+        while self.gen_total < A + N:
+            counts, win = b.noise_chunk()
+            allc = c.allgather_array(counts)
+            wins = c.allgather_tensor(win)
+            for r in range(c.world):   # chunk order: this round's chunk of rank 0, 1, ...
+                cum = np.concatenate([[0], np.cumsum(allc[r])]).astype(np.int64)
+                self.chunks.append((self.gen_total, cum, wins[r]))
+                self.gen_total += int(cum[-1])
+        a, e = A + k_off, A + k_off + n_loc
+        segs = []
+        for s0, cum, win in self.chunks:
+            if s0 + cum[-1] <= a or s0 >= e:
+                continue
+            p0 = max(0, int(np.searchsorted(cum, a - s0, side='right')) - 1)
+            for p in range(p0, self.P):
+                if s0 + cum[p] >= e:
+                    break
+                if cum[p + 1] > cum[p]:
+                    segs.append((win, p, s0 + int(cum[p])))
+        b.noise_fill(segs, a, e)
+        self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
 
 
 class DistSolve:
@@ -100,6 +158,8 @@ class DistSolve:
         self.max_pts = 0
         self.winner = None                      # (turn, global rank)
         self.counts = [comm.allgather_int(backend.n_local())]   # per turn: per-rank slice sizes
+        self.noise = ShardNoise(backend, comm) if use_heuristic else None
+        self.consumed = 0                       # accepted draws used so far (global)
 
     def offset(self, turn=None) -> int:
         cnt = self.counts[self.turn if turn is None else turn]
@@ -162,6 +222,9 @@ class DistSolve:
             self.done, self.winner = True, (self.turn, last)
             st.update(done=True, winner_rank=last)
             return st
+        if self.heur:
+            self.noise.prepare(self.consumed, N, k_off, n_loc)
+            self.consumed += N
         b.emit(k_off, N, off)
         K = min(N, self.W) if self.heur else N
         G = c.world
@@ -278,6 +341,9 @@ class HipBackend:
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_hist.argtypes = [vp, i32, vp, i32, vp]
         lib.sbd_eq_count.argtypes = [vp, u64, p64]
+        lib.sbd_noise_info.argtypes = [vp, vp]
+        lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
+        lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
         lib.sbd_partition.argtypes = [vp, i32, u64, i64, i32, vp, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
         lib.sbd_pack_kept.argtypes = [vp, vp, vp, vp, vp]
@@ -353,6 +419,26 @@ class HipBackend:
         n = self.C.c_int64()
         self._chk(self.lib.sbd_apply(self.h, back.data_ptr(), self.C.byref(n)), 'sbd_apply')
         return n.value
+
+    def noise_info(self):
+        out = np.zeros(4, np.uint64)
+        self._chk(self.lib.sbd_noise_info(self.h, out.ctypes.data), 'sbd_noise_info')
+        self.P = int(out[0])
+        return [int(x) for x in out]
+
+    def noise_chunk(self):
+        win = torch.empty(self.P * 624, dtype=torch.int32, device=self.device)
+        counts = np.zeros(self.P, np.uint32)
+        self._sync()
+        self._chk(self.lib.sbd_noise_chunk(self.h, win.data_ptr(), counts.ctypes.data), 'sbd_noise_chunk')
+        return counts.astype(np.int64), win
+
+    def noise_fill(self, segs, a, e):
+        self._sync()   # gathered windows are written by collectives on torch's stream
+        ptrs = np.array([w.data_ptr() + p * 624 * 4 for w, p, _ in segs], dtype=np.uint64)
+        acc0 = np.array([x for _, _, x in segs], dtype=np.uint64)
+        self._chk(self.lib.sbd_noise_fill(self.h, len(segs), ptrs.ctypes.data if len(segs) else None,
+                                          acc0.ctypes.data if len(segs) else None, int(a), int(e)), 'sbd_noise_fill')
 
     def emit(self, k_off, N, off):
         self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')

@@ -42,7 +42,7 @@ def _worker(rank, world, port, cfg, outdir):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     random.seed(cfg['seed'])
     st = random.getstate()[1]
-    b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st)
+    b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
     solve = DistSolve(b, Comm(torch.device('cpu')), goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                       beam_width=cfg['width'])
     trace = solve.run()
