@@ -457,65 +457,6 @@ __global__ __launch_bounds__(256) void k_survive(int64_t n, const Entry* __restr
     }
 }
 
-// ------------------------------------------------------------------ k_emit (wave per parent)
-template <int H>
-__global__ __launch_bounds__(256) void k_emit(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
-                                              const uint64_t* __restrict__ bhi, int64_t n,
-                                              const uint8_t* __restrict__ desc,
-                                              const unsigned long long* __restrict__ surv,
-                                              const uint32_t* __restrict__ off, uint64_t* __restrict__ nlo,
-                                              uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
-                                              uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
-                                              uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
-                                              uint32_t* __restrict__ err) {
-    __shared__ uint32_t card[NCARDS];
-    __shared__ uint32_t pat[4][NPAT_MAX];
-    __shared__ int32_t npat[4];
-    __shared__ uint64_t mlo[NCOL];
-    __shared__ uint32_t mhi[NCOL];
-    load_tables_lds(T, card, pat, npat, mlo, mhi);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = lanemask_lt();
-    const int64_t wg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t r = wg; r < n; r += nw) {
-        const uint64_t lo = blo[r], hi = bhi[r];
-        Derived d;
-        derive_lds(mlo, mhi, lo, hi, d);
-        const int bk = take_bucket(d);
-        uint32_t k = off[r];
-#pragma unroll
-        for (int pass = 0; pass < 3; pass++) {
-            const unsigned long long sm = surv[r * 3 + pass];
-            if (sm == 0) continue;
-            if ((sm >> lane) & 1ull) {
-                const int o = pass * 64 + lane;
-                const uint32_t kk = k + __popcll(sm & lt);
-                const int dsc = desc[r * MAX_CHILDREN + o];
-                uint64_t clo = lo, chi;
-                if (dsc < NCARDS) {
-                    chi = buy_child_hi(card[dsc], dsc, d, hi, &clo);
-                } else {
-                    uint32_t gf;
-                    take_child(pat[bk][dsc - NCARDS], d, &gf);
-                    chi = st_with_gems(hi, gf);
-                }
-                nlo[kk] = clo;
-                nhi[kk] = chi;
-                npar[kk] = par_base + (uint32_t)r;
-                if constexpr (H >= 0) {
-                    if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
-                    const int nv = ring[(ring_base + kk) & ring_mask];
-                    const double sc = score_of<H>(T->pw, *T, clo, chi, T->noise[nv - 1]);
-                    skey[kk] = (uint64_t)__double_as_longlong(sc);
-                }
-            }
-            k += __popcll(sm);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ survivors of the lost-marking path
 __global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long long* __restrict__ cand,
                                                   const unsigned long long* __restrict__ lost, uint32_t* __restrict__ cnt) {
