@@ -179,7 +179,7 @@ def main():
     if args.realistic:
         return run_realistic(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or os.environ.get('SB_FORCE_DIST') == '1':   # (diagnostic: sharded path at N=1)
         import bench_dist
         return bench_dist.main(args)
     per, elapsed, setup_turns = run_single(args)

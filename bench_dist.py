@@ -54,6 +54,10 @@ def main(args):
     raw = sum(p['n_raw'] for p in per)
     uniq = sum(p['n_unique'] for p in per)
     kept = sum(p['n_kept'] for p in per)
+    if rank == 0 and os.environ.get('SB_DIST_PHASES') == '1':
+        import sys
+        for p in per:
+            print('phases', p.get('phases'), file=sys.stderr, flush=True)
     if rank == 0:
         gbs = step_bytes(parents, raw, uniq, kept) / el_max / 1e9
         out = {

@@ -885,6 +885,7 @@ struct Engine {
     DBuf<uint64_t> nw;
     DBuf<uint64_t> cand_key, cand_tag;
     DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
+    DBuf<unsigned long long> own_lost;
     DBuf<uint8_t> digit;
 };
 
@@ -1239,10 +1240,11 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         }
         if (lg < 10 || lg > 32) throw HipError{hipErrorInvalidValue, "visited_log2 out of range [10, 32]"};
         const uint64_t cap = 1ull << lg;
-        E.tab_mask = cap - 1;
-        SB_HIP(hipMalloc((void**)&E.tab, cap * sizeof(Entry)));
-        SB_HIP(hipMemsetAsync(E.tab, 0xFF, cap * sizeof(Entry), E.s));
-        const bool distm = cfg->world_size > 1;
+        const bool distm = cfg->world_size > 1 || (cfg->flags & 2);   // bit 1: sharded protocol at any world size
+        const uint64_t tcap = distm ? 1024 : cap;   // sharded: the trail lives in the owner shards (E.own)
+        E.tab_mask = tcap - 1;
+        SB_HIP(hipMalloc((void**)&E.tab, tcap * sizeof(Entry)));
+        SB_HIP(hipMemsetAsync(E.tab, 0xFF, tcap * sizeof(Entry), E.s));
         if (distm) {
             if (cfg->rank < 0 || cfg->rank >= cfg->world_size || cfg->world_size > 64)
                 throw HipError{hipErrorInvalidValue, "bad rank / world_size (<= 64)"};
@@ -1443,6 +1445,7 @@ void sb_destroy(sb_engine* h) {
     E.cand_ro.release();
     E.cand_pos.release();
     E.own_slot.release();
+    E.own_lost.release();
     E.part_hist.release();
     E.digit.release();
     if (E.d_tables) (void)hipFree(E.d_tables);

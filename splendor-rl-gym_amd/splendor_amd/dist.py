@@ -6,11 +6,12 @@ positions [off_r, off_r + n_r)), so the (parent rank, ordinal) order that decide
 src/solver.py:452-456) stay global.  One step, per rank:
 
   goal      local first rank per pts -> global (+off) -> all_reduce(MIN)  (src/solver.py:438-445)
-  expand    successors of the local parents; a rank-local visited table removes children this rank
-            has generated before (they are already in the global trail) and local same-turn repeats
-  dedup     all_to_all of (key, global tag) to the key's owner (mix64(key) top bits mod world);
-            the owner's shard of the global visited set claims by atomicMin of the tag and answers
-            one byte per record (first occurrence or not); all_to_all back
+  expand    every successor of the local parents becomes a record (key, owner = mix64(key) top bits
+            mod world), grouped by owner in (parent, ordinal) order
+  dedup     all_to_all of the keys to their owners; records arrive source rank by source rank, so
+            the record index at the owner is the global (parent rank, ordinal) order: the owner's
+            shard of the global visited set claims with tag = turn | record index and answers one
+            byte per record (first occurrence or not); all_to_all back
   offsets   all_gather of per-rank unique counts -> this rank's next_queue offset k_off
   emit      survivors' states + scores; noise = accepted MT draw (consumed + k_off + k): every rank
             runs the same jump-ahead MT19937 stream
@@ -26,9 +27,14 @@ reference backend).  All results are bit-identical to the single-GPU engine and 
 """
 from __future__ import annotations
 
+import os
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
+
+_PHASES = os.environ.get('SB_DIST_PHASES') == '1'   # diagnostic: host wall time per protocol phase
 
 NONE32 = 0xFFFFFFFF
 BIG = (1 << 62)
@@ -189,15 +195,24 @@ class DistSolve:
         return win
 
     # ------------------------------------------------------------ one step (src/solver.py:434-457)
+    def _mark(self, st, name):
+        if _PHASES:
+            torch.cuda.synchronize() if torch.cuda.is_available() else None
+            t = time.perf_counter()
+            st.setdefault('phases', {})[name] = round((t - self._t) * 1e3, 3)
+            self._t = t
+
     def step(self) -> dict:
         c, b = self.c, self.b
         st = {'turn': self.turn, 'records': [], 'done': False}
+        self._t = time.perf_counter()
         cnt = self.counts[self.turn]
         st['n_parents'] = int(cnt.sum())
         if self.done:
             st['done'] = True
             return st
         win = self._goal_check(st)
+        self._mark(st, 'goal')
         if win >= 0:
             self.done, self.winner = True, (self.turn, win)
             st.update(done=True, winner_rank=win)
@@ -206,13 +221,14 @@ class DistSolve:
         # local expansion + local filter; candidate records grouped by owner
         owner_counts, n_raw = b.expand(off, self.turn, c.world)
         st['n_raw'] = int(c.allreduce(np.array([n_raw]), dist.ReduceOp.SUM)[0])
-        send_key, send_tag = b.pack()
+        self._mark(st, 'expand')
+        send_key = b.pack()
         recv_counts = c.alltoall_counts(owner_counts)
         rkey = c.alltoall(send_key, owner_counts, recv_counts)
-        rtag = c.alltoall(send_tag, owner_counts, recv_counts)
-        ret = b.owner_claim(rkey, rtag, self.turn)
+        ret = b.owner_claim(rkey, self.turn)
         back = c.alltoall(ret, recv_counts, owner_counts)
         n_loc = b.apply(back)
+        self._mark(st, 'dedup_exchange')
         all_n = c.allgather_int(n_loc)
         k_off = int(all_n[:c.rank].sum())
         N = int(all_n.sum())
@@ -225,7 +241,9 @@ class DistSolve:
         if self.heur:
             self.noise.prepare(self.consumed, N, k_off, n_loc)
             self.consumed += N
+        self._mark(st, 'noise')
         b.emit(k_off, N, off)
+        self._mark(st, 'emit')
         K = min(N, self.W) if self.heur else N
         G = c.world
         if self.heur:
@@ -246,6 +264,7 @@ class DistSolve:
             dest_counts = b.partition(top, T, G)
         else:
             dest_counts = b.partition_bfs(k_off, N, G)
+        self._mark(st, 'select')
         lo, hi, par, key = b.pack_kept()
         recv = c.alltoall_counts(dest_counts)
         rlo = c.alltoall(lo, dest_counts, recv)
@@ -254,6 +273,7 @@ class DistSolve:
         rkey = c.alltoall(key, dest_counts, recv)
         b.receive(rlo, rhi, rpar, rkey, self.heur)
         self.counts.append(c.allgather_int(b.n_local()))
+        self._mark(st, 'rebalance')
         self.turn += 1
         st['n_kept'] = int(self.counts[-1].sum())
         return st
@@ -261,6 +281,8 @@ class DistSolve:
     def _multiselect(self, positions):
         """Global key at each 1-based position of the (score desc) order, 8 MSB passes of 8 bits."""
         nb = len(positions)
+        if nb == 0:   # world 1 and nothing to prune
+            return [], []
         pref = np.zeros(nb, dtype=np.uint64)
         need = np.array(positions, dtype=np.int64)
         for p in range(8):
@@ -320,7 +342,7 @@ class HipBackend:
         torch.cuda.set_device(self.device)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=0, world_size=int(world), rank=int(rank))
+                         flags=2, world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
         L.check(self.lib.sb_create(C.byref(cfg), st, int(root[0]), int(root[1]), C.byref(h)), 'sb_create')
@@ -403,14 +425,14 @@ class HipBackend:
 
     def pack(self):
         n = int(self.owner_counts.sum())
-        key, tag = self._empty(n), self._empty(n)
-        self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), tag.data_ptr()), 'sbd_pack')
-        return key, tag
+        key = self._empty(n)
+        self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), None), 'sbd_pack')
+        return key
 
-    def owner_claim(self, rkey, rtag, turn):
+    def owner_claim(self, rkey, turn):
         self._sync()
         ret = self._empty(rkey.numel(), torch.uint8)
-        self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr(), rtag.data_ptr(), rkey.numel(), ret.data_ptr()),
+        self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr(), None, rkey.numel(), ret.data_ptr()),
                   'sbd_owner_claim')
         return ret
 
