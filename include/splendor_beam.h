@@ -164,8 +164,15 @@ int sbd_noise_info(sb_engine* e, uint64_t* out4);
 int sbd_noise_chunk(sb_engine* e, void* win_out, uint32_t* counts_host);
 int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
 
-/* radix-select pass: histogram of the next 8 bits of keys whose top `bits` bits equal pref[j] */
-int sbd_hist(sb_engine* e, int32_t nb, const uint64_t* pref_host, int32_t bits, int64_t* hist_host);
+/* Joint select helpers (dist.py): sbd_key_range = min/max of this rank's score keys of the turn;
+ * sbd_sel_hist = histograms (nb x 2^d, int64) of the digit [hi-d, hi) over the keys (src 0) or the
+ * candidates (src 1) whose bits above hi equal one of the nb distinct prefixes; sbd_sel_compact =
+ * keep as candidates the keys whose bits above hi equal one of the prefixes. */
+int sbd_key_range(sb_engine* e, uint64_t* out2);
+int sbd_sel_hist(sb_engine* e, int32_t src, int32_t nb, const uint64_t* pref_host, int32_t hi, int32_t d,
+                 int64_t* hist_host);
+int sbd_sel_compact(sb_engine* e, int32_t nb, const uint64_t* pref_host, int32_t hi);
+
 int sbd_eq_count(sb_engine* e, uint64_t T, int64_t* out);
 /* kept = key > T or (key == T and local tie index < quota) [if has_top]; destination range =
  * #{j : key < split_j}; dest_counts[world] */

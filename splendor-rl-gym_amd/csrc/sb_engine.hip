@@ -886,6 +886,7 @@ struct Engine {
     DBuf<uint64_t> cand_key, cand_tag;
     DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
     DBuf<unsigned long long> own_lost;
+    DBuf<uint64_t> dsel, dsel_c;          // joint select: prefixes / histograms, candidate keys
     DBuf<uint8_t> digit;
 };
 
@@ -1446,6 +1447,8 @@ void sb_destroy(sb_engine* h) {
     E.cand_pos.release();
     E.own_slot.release();
     E.own_lost.release();
+    E.dsel.release();
+    E.dsel_c.release();
     E.part_hist.release();
     E.digit.release();
     if (E.d_tables) (void)hipFree(E.d_tables);

@@ -279,23 +279,39 @@ class DistSolve:
         return st
 
     def _multiselect(self, positions):
-        """Global key at each 1-based position of the (score desc) order, 8 MSB passes of 8 bits."""
+        """Global key at each 1-based position of the (score desc) order and how many of its ties
+        precede the position: MSB radix select over 10-bit digits below the bits common to every
+        key (global min/max), one all_reduce(SUM) of the histograms per pass (one per distinct
+        prefix); after the first pass each rank keeps only its keys in the chosen buckets."""
+        c, b = self.c, self.b
         nb = len(positions)
         if nb == 0:   # world 1 and nothing to prune
             return [], []
-        pref = np.zeros(nb, dtype=np.uint64)
-        need = np.array(positions, dtype=np.int64)
-        for p in range(8):
-            H = self.c.allreduce(self.b.hist(pref, 8 * p), dist.ReduceOp.SUM).reshape(nb, 256)
+        rng = c.allgather_array(np.array([_u64_to_i64(x) for x in b.key_range()], dtype=np.int64))
+        mins = [x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 0].tolist()]
+        maxs = [x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 1].tolist()]
+        mn, mx = min(mins), max(maxs)
+        hi = (mn ^ mx).bit_length()
+        pref = [mn >> hi if hi < 64 else 0] * nb
+        need = [int(x) for x in positions]
+        src = 0
+        while hi > 0:
+            d = min(10, hi)
+            uniq = sorted(set(pref))
+            H = c.allreduce(b.sel_hist(src, uniq, hi, d), dist.ReduceOp.SUM).reshape(len(uniq), 1 << d)
             for j in range(nb):
-                cum = 0
-                d = 255
-                while d > 0 and cum + H[j, d] < need[j]:
-                    cum += int(H[j, d])
-                    d -= 1
+                h = H[uniq.index(pref[j])]
+                cum, dg = 0, (1 << d) - 1
+                while dg > 0 and cum + int(h[dg]) < need[j]:
+                    cum += int(h[dg])
+                    dg -= 1
                 need[j] -= cum
-                pref[j] = (int(pref[j]) << 8 | d) & 0xFFFFFFFFFFFFFFFF
-        return [int(x) for x in pref], [int(x) for x in need]
+                pref[j] = (pref[j] << d) | dg
+            hi -= d
+            if src == 0 and hi > 0:
+                b.sel_compact(sorted(set(pref)), hi)
+                src = 1
+        return pref, need
 
     def run(self, max_turns=10_000):
         trace = []
@@ -361,8 +377,10 @@ class HipBackend:
         lib.sbd_owner_claim.argtypes = [vp, vp, vp, i64, vp]
         lib.sbd_apply.argtypes = [vp, vp, p64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
-        lib.sbd_hist.argtypes = [vp, i32, vp, i32, vp]
         lib.sbd_eq_count.argtypes = [vp, u64, p64]
+        lib.sbd_key_range.argtypes = [vp, vp]
+        lib.sbd_sel_hist.argtypes = [vp, i32, i32, vp, i32, i32, vp]
+        lib.sbd_sel_compact.argtypes = [vp, i32, vp, i32]
         lib.sbd_noise_info.argtypes = [vp, vp]
         lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
@@ -465,12 +483,21 @@ class HipBackend:
     def emit(self, k_off, N, off):
         self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')
 
-    def hist(self, pref, bits):
-        nb = len(pref)
-        p = np.ascontiguousarray(np.asarray(pref, dtype=np.uint64))
-        out = np.zeros(nb * 256, np.int64)
-        self._chk(self.lib.sbd_hist(self.h, nb, p.ctypes.data, int(bits), out.ctypes.data), 'sbd_hist')
+    def key_range(self):
+        out = np.zeros(2, np.uint64)
+        self._chk(self.lib.sbd_key_range(self.h, out.ctypes.data), 'sbd_key_range')
+        return [int(out[0]), int(out[1])]
+
+    def sel_hist(self, src, prefs, hi, d):
+        p = np.ascontiguousarray(np.array(prefs, dtype=np.uint64))
+        out = np.zeros(len(prefs) << d, np.int64)
+        self._chk(self.lib.sbd_sel_hist(self.h, int(src), len(prefs), p.ctypes.data, int(hi), int(d), out.ctypes.data),
+                  'sbd_sel_hist')
         return out
+
+    def sel_compact(self, prefs, hi):
+        p = np.ascontiguousarray(np.array(prefs, dtype=np.uint64))
+        self._chk(self.lib.sbd_sel_compact(self.h, len(prefs), p.ctypes.data, int(hi)), 'sbd_sel_compact')
 
     def eq_count(self, T):
         n = self.C.c_int64()
