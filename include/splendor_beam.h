@@ -157,11 +157,13 @@ int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
 /* Sharded noise stream (world > 1, heuristic): rank r owns MT19937 chunks c = r (mod world), each
  * P producer segments of twists*624 words.  sbd_noise_info: [P, twists, accepted values in the lead
  * block, consumed].  sbd_noise_chunk: the P windows (624 u32 each, device buffer win_out) of the
- * rank's next owned chunk and its per-producer accepted counts (host).  sbd_noise_fill: regenerate
+ * rank's next owned chunk and its per-producer accepted counts (P u32, device buffer counts_out),
+ * launched asynchronously (sbd_noise_sync waits).  sbd_noise_fill: regenerate
  * nseg producer segments (device window addresses, global index of each one's first accepted draw)
  * and store the accepted values with global index in [a, b) for this rank's emission. */
 int sbd_noise_info(sb_engine* e, uint64_t* out4);
-int sbd_noise_chunk(sb_engine* e, void* win_out, uint32_t* counts_host);
+int sbd_noise_chunk(sb_engine* e, void* win_out, void* counts_out);   /* device buffers; asynchronous */
+int sbd_noise_sync(sb_engine* e);                                       /* wait for sbd_noise_chunk */
 int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
 
 /* Joint select helpers (dist.py): sbd_key_range = min/max of this rank's score keys of the turn;

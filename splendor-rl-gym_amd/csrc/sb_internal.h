@@ -162,9 +162,10 @@ void noise_ensure(NoiseStream& ns, uint64_t need, hipStream_t st);
 void noise_free(NoiseStream& ns);
 // Sharded stream (world > 1): chunks c = rank (mod world) are this rank's.  setup jumps the producers
 // to chunk `rank`; chunk() copies the P producer windows of the next owned chunk to d_win_out and
-// returns its per-producer accepted counts; fill() regenerates producer segments into the ring.
+// writes its per-producer accepted counts to d_counts (asynchronously on st); fill() regenerates
+// producer segments into the ring.
 void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st);
-void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* h_counts, hipStream_t st);
+void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* d_counts, hipStream_t st);
 void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,
                       hipStream_t st);
 void noise_mt_state(NoiseStream& ns, uint32_t* out625);

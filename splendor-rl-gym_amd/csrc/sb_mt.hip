@@ -399,17 +399,15 @@ void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st) {
     ns.sharded = true;
 }
 
-void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* h_counts, hipStream_t st) {
+void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* d_counts, hipStream_t st) {
     MTProducers& pr = ns.prod;
     if (pr.chunk > 0)
         hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
     SB_HIP(hipMemcpyAsync(d_win_out, pr.d_win, (size_t)pr.P * 624 * 4, hipMemcpyDeviceToDevice, st));
-    ns.scan.tiles.ensure((size_t)pr.P);
     hipLaunchKernelGGL(k_mt_gen_par<2>, dim3(pr.P), dim3(640), 0, st, pr.d_win, (uint32_t*)nullptr, (uint8_t*)nullptr,
-                       ns.scan.tiles.p, pr.twists);
-    SB_HIP(hipMemcpyAsync(h_counts, ns.scan.tiles.p, (size_t)pr.P * 4, hipMemcpyDeviceToHost, st));
-    SB_HIP(hipStreamSynchronize(st));
-    pr.chunk++;
+                       d_counts, pr.twists);
+    SB_HIP(hipGetLastError());
+    pr.chunk++;   // asynchronous: the caller synchronises st before using d_win_out / d_counts
 }
 
 void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,

@@ -98,9 +98,25 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
     const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
     const uint64_t d = sh < SEL_D ? sh : SEL_D;
     const uint64_t dmask = (1ull << d) - 1;
-    for (int64_t i = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * TK_NT) {
-        const uint64_t k = keys[i];
-        if (hi_bits(k, sh) == prefix) atomicAdd(&h[w][(k >> (sh - d)) & dmask], 1u);
+    const uint64_t lt = lanemask_lt();
+    for (int64_t i0 = (int64_t)blockIdx.x * TK_NT; i0 < n; i0 += (int64_t)gridDim.x * TK_NT) {
+        const int64_t i = i0 + threadIdx.x;
+        int b = -1;
+        if (i < n) {
+            const uint64_t k = keys[i];
+            if (hi_bits(k, sh) == prefix) b = (int)((k >> (sh - d)) & dmask);
+        }
+        // scores cluster: lanes sharing the first active lane's bin add once (wave-aggregated)
+        const uint64_t act = __ballot(b >= 0);
+        if (act) {
+            const int b0 = __shfl(b, __builtin_ctzll(act), 64);
+            const uint64_t same = __ballot(b == b0);
+            if (b == b0) {
+                if ((same & lt) == 0) atomicAdd(&h[w][b0], (uint32_t)__popcll(same));
+            } else if (b >= 0) {
+                atomicAdd(&h[w][b], 1u);
+            }
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < SEL_BINS; b += TK_NT) {

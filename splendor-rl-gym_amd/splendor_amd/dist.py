@@ -123,18 +123,29 @@ class ShardNoise:
         self.P = int(info[0])
         self.gen_total = int(info[2])   # accepted draws available (global index), the lead block first
         self.chunks = []                # (first global accepted index, cumulative counts (P+1), windows)
+        self.pending = None             # (counts, windows) of a round launched but not yet gathered
+
+    def _collect(self):
+        """All-gather the round launched by noise_chunk (every rank one chunk)."""
+        c, b = self.c, self.b
+        counts, win = self.pending
+        self.pending = None
+        b.noise_sync()
+        allc = [x.cpu().numpy().astype(np.int64) for x in c.allgather_tensor(counts)]
+        wins = c.allgather_tensor(win)
+        for r in range(c.world):   # chunk order: this round's chunk of rank 0, 1, ...
+            cum = np.concatenate([[0], np.cumsum(allc[r])]).astype(np.int64)
+            self.chunks.append((self.gen_total, cum, wins[r]))
+            self.gen_total += int(cum[-1])
 
     def prepare(self, A: int, N: int, k_off: int, n_loc: int):
         """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission."""
         c, b = self.c, self.b
+        if self.pending is not None:
+            self._collect()
         while self.gen_total < A + N:
-            counts, win = b.noise_chunk()
-            allc = c.allgather_array(counts)
-            wins = c.allgather_tensor(win)
-            for r in range(c.world):   # chunk order: this round's chunk of rank 0, 1, ...
-                cum = np.concatenate([[0], np.cumsum(allc[r])]).astype(np.int64)
-                self.chunks.append((self.gen_total, cum, wins[r]))
-                self.gen_total += int(cum[-1])
+            self.pending = b.noise_chunk()
+            self._collect()
         a, e = A + k_off, A + k_off + n_loc
         segs = []
         for s0, cum, win in self.chunks:
@@ -148,6 +159,9 @@ class ShardNoise:
                     segs.append((win, p, s0 + int(cum[p])))
         b.noise_fill(segs, a, e)
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
+        # next round in the background (side stream) while the step goes on; gathered next turn
+        if self.gen_total < A + N + 2 * N:
+            self.pending = b.noise_chunk()
 
 
 class DistSolve:
@@ -383,6 +397,7 @@ class HipBackend:
         lib.sbd_sel_compact.argtypes = [vp, i32, vp, i32]
         lib.sbd_noise_info.argtypes = [vp, vp]
         lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
+        lib.sbd_noise_sync.argtypes = [vp]
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
         lib.sbd_partition.argtypes = [vp, i32, u64, i64, i32, vp, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
@@ -468,10 +483,12 @@ class HipBackend:
 
     def noise_chunk(self):
         win = torch.empty(self.P * 624, dtype=torch.int32, device=self.device)
-        counts = np.zeros(self.P, np.uint32)
-        self._sync()
-        self._chk(self.lib.sbd_noise_chunk(self.h, win.data_ptr(), counts.ctypes.data), 'sbd_noise_chunk')
-        return counts.astype(np.int64), win
+        counts = torch.empty(self.P, dtype=torch.int32, device=self.device)
+        self._chk(self.lib.sbd_noise_chunk(self.h, win.data_ptr(), counts.data_ptr()), 'sbd_noise_chunk')
+        return counts, win
+
+    def noise_sync(self):
+        self._chk(self.lib.sbd_noise_sync(self.h), 'sbd_noise_sync')
 
     def noise_fill(self, segs, a, e):
         self._sync()   # gathered windows are written by collectives on torch's stream
