@@ -887,6 +887,7 @@ struct Engine {
     DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
     DBuf<unsigned long long> own_lost;
     DBuf<uint64_t> dsel, dsel_c;          // joint select: prefixes / histograms, candidate keys
+    DBuf<uint32_t> dsel_t;                // joint select: compaction tile offsets
     DBuf<uint8_t> digit;
 };
 
@@ -1449,6 +1450,7 @@ void sb_destroy(sb_engine* h) {
     E.own_lost.release();
     E.dsel.release();
     E.dsel_c.release();
+    E.dsel_t.release();
     E.part_hist.release();
     E.digit.release();
     if (E.d_tables) (void)hipFree(E.d_tables);

@@ -237,9 +237,12 @@ class DistSolve:
         st['n_raw'] = int(c.allreduce(np.array([n_raw]), dist.ReduceOp.SUM)[0])
         self._mark(st, 'expand')
         send_key = b.pack()
+        self._mark(st, 'pack')
         recv_counts = c.alltoall_counts(owner_counts)
         rkey = c.alltoall(send_key, owner_counts, recv_counts)
+        self._mark(st, 'a2a_keys')
         ret = b.owner_claim(rkey, self.turn)
+        self._mark(st, 'claim')
         back = c.alltoall(ret, recv_counts, owner_counts)
         n_loc = b.apply(back)
         self._mark(st, 'dedup_exchange')
@@ -266,7 +269,8 @@ class DistSolve:
                 pos.append(self.W)
             splits = [max(1, -(-j * K // G)) for j in range(1, G)]
             pos += splits
-            T, need = self._multiselect(pos)
+            T, need = self._multiselect(pos, st)
+            self._mark(st, 'sel_passes')
             top = None
             if N > self.W:
                 t0, m0 = T[0], need[0]
@@ -275,16 +279,19 @@ class DistSolve:
                 quota = max(0, min(m0 - before, int(eq[c.rank])))
                 top = (t0, quota)
                 T = T[1:]
+            self._mark(st, 'sel_eq')
             dest_counts = b.partition(top, T, G)
         else:
             dest_counts = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
         lo, hi, par, key = b.pack_kept()
+        self._mark(st, 'pack_kept')
         recv = c.alltoall_counts(dest_counts)
         rlo = c.alltoall(lo, dest_counts, recv)
         rhi = c.alltoall(hi, dest_counts, recv)
         rpar = c.alltoall(par, dest_counts, recv)
         rkey = c.alltoall(key, dest_counts, recv)
+        self._mark(st, 'a2a_kept')
         b.receive(rlo, rhi, rpar, rkey, self.heur)
         self.counts.append(c.allgather_int(b.n_local()))
         self._mark(st, 'rebalance')
@@ -292,7 +299,7 @@ class DistSolve:
         st['n_kept'] = int(self.counts[-1].sum())
         return st
 
-    def _multiselect(self, positions):
+    def _multiselect(self, positions, st=None):
         """Global key at each 1-based position of the (score desc) order and how many of its ties
         precede the position: MSB radix select over 10-bit digits below the bits common to every
         key (global min/max), one all_reduce(SUM) of the histograms per pass (one per distinct
@@ -312,7 +319,12 @@ class DistSolve:
         while hi > 0:
             d = min(10, hi)
             uniq = sorted(set(pref))
-            H = c.allreduce(b.sel_hist(src, uniq, hi, d), dist.ReduceOp.SUM).reshape(len(uniq), 1 << d)
+            h_loc = b.sel_hist(src, uniq, hi, d)
+            if st is not None:
+                self._mark(st, f'hist{hi}')
+            H = c.allreduce(h_loc, dist.ReduceOp.SUM).reshape(len(uniq), 1 << d)
+            if st is not None:
+                self._mark(st, f'ar{hi}')
             for j in range(nb):
                 h = H[uniq.index(pref[j])]
                 cum, dg = 0, (1 << d) - 1
