@@ -161,6 +161,9 @@ int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
  * launched asynchronously (sbd_noise_sync waits).  sbd_noise_fill: regenerate
  * nseg producer segments (device window addresses, global index of each one's first accepted draw)
  * and store the accepted values with global index in [a, b) for this rank's emission. */
+/* Run the engine's step work on the caller's stream (e.g. torch.cuda.current_stream(), which the RCCL
+ * collectives use): exchanges and kernels are then ordered without host synchronisation. */
+int sbd_set_stream(sb_engine* e, void* stream);
 int sbd_noise_info(sb_engine* e, uint64_t* out4);
 int sbd_noise_chunk(sb_engine* e, void* win_out, void* counts_out);   /* device buffers; asynchronous */
 int sbd_noise_sync(sb_engine* e);                                       /* wait for sbd_noise_chunk */

@@ -843,6 +843,7 @@ struct Engine {
     sb_config cfg{};
     int dev = 0;
     hipStream_t s = nullptr, s_mt = nullptr;
+    bool s_external = false;                // sbd_set_stream: the caller's stream (not destroyed here)
     Tables* d_tables = nullptr;
     Entry* tab = nullptr;
     uint64_t tab_mask = 0;
@@ -1462,7 +1463,7 @@ void sb_destroy(sb_engine* h) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : E.tev)
         if (e) (void)hipEventDestroy(e);
-    if (E.s) (void)hipStreamDestroy(E.s);
+    if (E.s && !E.s_external) (void)hipStreamDestroy(E.s);
     if (E.s_mt) (void)hipStreamDestroy(E.s_mt);
     delete h;
 }

@@ -368,8 +368,9 @@ class HipBackend:
     """Per-rank primitives on the MI355X engine (libsplendor_beam.so, sbd_* entry points).
 
     Exchange buffers are torch tensors on this rank's device, handed to the engine by device
-    pointer; every sbd_* call returns after its device work completed, and the tensors written by
-    collectives are synchronised before the engine reads them.
+    pointer.  The engine runs on torch's current stream (sbd_set_stream), the stream the
+    collectives use, so kernels and exchanges are ordered on the device; the host waits only where
+    it needs a value (counts that size an all_to_all, the goal table).
     """
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
@@ -390,6 +391,9 @@ class HipBackend:
         L.check(self.lib.sb_create(C.byref(cfg), st, int(root[0]), int(root[1]), C.byref(h)), 'sb_create')
         self.h = h
         self.world = world
+        # one stream for the engine's kernels and the collectives: ordered without host syncs
+        self.stream = torch.cuda.current_stream(self.device)
+        L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
 
     def _bind(self):
         C, lib = self.C, self.lib
@@ -407,6 +411,7 @@ class HipBackend:
         lib.sbd_key_range.argtypes = [vp, vp]
         lib.sbd_sel_hist.argtypes = [vp, i32, i32, vp, i32, i32, vp]
         lib.sbd_sel_compact.argtypes = [vp, i32, vp, i32]
+        lib.sbd_set_stream.argtypes = [vp, vp]
         lib.sbd_noise_info.argtypes = [vp, vp]
         lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
         lib.sbd_noise_sync.argtypes = [vp]
@@ -475,14 +480,12 @@ class HipBackend:
         return key
 
     def owner_claim(self, rkey, turn):
-        self._sync()
         ret = self._empty(rkey.numel(), torch.uint8)
         self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr(), None, rkey.numel(), ret.data_ptr()),
                   'sbd_owner_claim')
         return ret
 
     def apply(self, back):
-        self._sync()
         n = self.C.c_int64()
         self._chk(self.lib.sbd_apply(self.h, back.data_ptr(), self.C.byref(n)), 'sbd_apply')
         return n.value
@@ -503,7 +506,6 @@ class HipBackend:
         self._chk(self.lib.sbd_noise_sync(self.h), 'sbd_noise_sync')
 
     def noise_fill(self, segs, a, e):
-        self._sync()   # gathered windows are written by collectives on torch's stream
         ptrs = np.array([w.data_ptr() + p * 624 * 4 for w, p, _ in segs], dtype=np.uint64)
         acc0 = np.array([x for _, _, x in segs], dtype=np.uint64)
         self._chk(self.lib.sbd_noise_fill(self.h, len(segs), ptrs.ctypes.data if len(segs) else None,
@@ -558,6 +560,5 @@ class HipBackend:
         return lo, hi, par, key
 
     def receive(self, lo, hi, par, key, heur):
-        self._sync()
         self._chk(self.lib.sbd_receive(self.h, lo.data_ptr(), hi.data_ptr(), par.data_ptr(), key.data_ptr(),
                                        lo.numel(), int(bool(heur))), 'sbd_receive')
