@@ -169,20 +169,24 @@ int sbd_noise_chunk(sb_engine* e, void* win_out, void* counts_out);   /* device 
 int sbd_noise_sync(sb_engine* e);                                       /* wait for sbd_noise_chunk */
 int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
 
-/* Joint select helpers (dist.py): sbd_key_range = min/max of this rank's score keys of the turn;
- * sbd_sel_hist = histograms (nb x 2^d, int64) of the digit [hi-d, hi) over the keys (src 0) or the
- * candidates (src 1) whose bits above hi equal one of the nb distinct prefixes; sbd_sel_compact =
- * keep as candidates the keys whose bits above hi equal one of the prefixes. */
+/* Joint select on the device (dist.py _multiselect): sbd_key_range = min/max of this rank's score keys
+ * of the turn; sbd_sel_begin = select state for npos positions (1-based ranks in score-descending
+ * order) below the bits common to [kmin, kmax]; per pass: sbd_sel_hist (16 x 1024 int64 histogram of
+ * the next 10-bit digit per distinct prefix into hist_dev, over the keys (src 0) or the candidates
+ * (src 1)), an all_reduce(SUM) of hist_dev by the caller on the same stream, sbd_sel_pick; after the
+ * first pass sbd_sel_compact keeps the keys of the chosen buckets as candidates.  sbd_sel_eq: count of
+ * keys equal to position 0's key (int64 at eq_dev) for the all_gather of the keep boundary's ties. */
 int sbd_key_range(sb_engine* e, uint64_t* out2);
-int sbd_sel_hist(sb_engine* e, int32_t src, int32_t nb, const uint64_t* pref_host, int32_t hi, int32_t d,
-                 int64_t* hist_host);
-int sbd_sel_compact(sb_engine* e, int32_t nb, const uint64_t* pref_host, int32_t hi);
-
-int sbd_eq_count(sb_engine* e, uint64_t T, int64_t* out);
-/* kept = key > T or (key == T and local tie index < quota) [if has_top]; destination range =
- * #{j : key < split_j}; dest_counts[world] */
-int sbd_partition(sb_engine* e, int32_t has_top, uint64_t T, int64_t quota, int32_t nsplit,
-                  const uint64_t* splits_host, int32_t world, int64_t* dest_counts);
+int sbd_sel_begin(sb_engine* e, int32_t npos, const int64_t* positions, uint64_t kmin, uint64_t kmax);
+int sbd_sel_hist(sb_engine* e, int32_t src, void* hist_dev);
+int sbd_sel_pick(sb_engine* e, const void* hist_dev);
+int sbd_sel_compact(sb_engine* e);
+int sbd_sel_eq(sb_engine* e, void* eq_dev);
+/* kept = key > T or (key == T and global tie index < its position) [if has_top; T = position 0's key,
+ * eq_all_dev = every rank's tie count]; destination range = #{j : key < split_j} (splits = the next
+ * nsplit positions' keys); dest_counts[world] */
+int sbd_partition(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t nsplit, int32_t world,
+                  int64_t* dest_counts);
 int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, int64_t* dest_counts);
 /* kept records grouped by destination, next_queue order inside a group */
 int sbd_pack_kept(sb_engine* e, uint64_t* d_lo, uint64_t* d_hi, uint64_t* d_par, uint64_t* d_key);

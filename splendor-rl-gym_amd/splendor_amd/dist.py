@@ -79,6 +79,15 @@ class Comm:
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
+    def allreduce_tensor(self, t: torch.Tensor):
+        """In-place SUM over ranks of a tensor on this rank's device."""
+        if self.cpu_coll:
+            x = t.cpu()
+            dist.all_reduce(x)
+            t.copy_(x.to(t.device))
+        else:
+            dist.all_reduce(t)
+
     def allgather_array(self, arr: np.ndarray) -> np.ndarray:
         """(world, len) int64 array of every rank's equal-length int vector."""
         t = self._to(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device))
@@ -264,23 +273,16 @@ class DistSolve:
         K = min(N, self.W) if self.heur else N
         G = c.world
         if self.heur:
-            pos = []
-            if N > self.W:
-                pos.append(self.W)
-            splits = [max(1, -(-j * K // G)) for j in range(1, G)]
-            pos += splits
-            T, need = self._multiselect(pos, st)
-            self._mark(st, 'sel_passes')
-            top = None
-            if N > self.W:
-                t0, m0 = T[0], need[0]
-                eq = c.allgather_int(b.eq_count(t0))
-                before = int(eq[:c.rank].sum())
-                quota = max(0, min(m0 - before, int(eq[c.rank])))
-                top = (t0, quota)
-                T = T[1:]
+            has_top = N > self.W
+            pos = ([self.W] if has_top else []) + [max(1, -(-j * K // G)) for j in range(1, G)]
+            eq_all = None
+            if pos:
+                self._multiselect(pos, st)
+                self._mark(st, 'sel_passes')
+                if has_top:
+                    eq_all = torch.cat(c.allgather_tensor(b.sel_eq()))
             self._mark(st, 'sel_eq')
-            dest_counts = b.partition(top, T, G)
+            dest_counts = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
         else:
             dest_counts = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
@@ -301,43 +303,24 @@ class DistSolve:
 
     def _multiselect(self, positions, st=None):
         """Global key at each 1-based position of the (score desc) order and how many of its ties
-        precede the position: MSB radix select over 10-bit digits below the bits common to every
-        key (global min/max), one all_reduce(SUM) of the histograms per pass (one per distinct
-        prefix); after the first pass each rank keeps only its keys in the chosen buckets."""
+        precede the position, left in the backend's select state: MSB radix select over 10-bit
+        digits below the bits common to every key (global min/max); per pass a histogram per
+        distinct prefix, all_reduce(SUM) on the device, a pick kernel; after the first pass each
+        rank keeps only its keys in the chosen buckets.  The passes are enqueued without waiting."""
         c, b = self.c, self.b
-        nb = len(positions)
-        if nb == 0:   # world 1 and nothing to prune
-            return [], []
         rng = c.allgather_array(np.array([_u64_to_i64(x) for x in b.key_range()], dtype=np.int64))
-        mins = [x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 0].tolist()]
-        maxs = [x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 1].tolist()]
-        mn, mx = min(mins), max(maxs)
-        hi = (mn ^ mx).bit_length()
-        pref = [mn >> hi if hi < 64 else 0] * nb
-        need = [int(x) for x in positions]
+        mn = min(x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 0].tolist())
+        mx = max(x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 1].tolist())
+        b.sel_begin(positions, mn, mx)
+        passes = -(-(mn ^ mx).bit_length() // 10)
         src = 0
-        while hi > 0:
-            d = min(10, hi)
-            uniq = sorted(set(pref))
-            h_loc = b.sel_hist(src, uniq, hi, d)
-            if st is not None:
-                self._mark(st, f'hist{hi}')
-            H = c.allreduce(h_loc, dist.ReduceOp.SUM).reshape(len(uniq), 1 << d)
-            if st is not None:
-                self._mark(st, f'ar{hi}')
-            for j in range(nb):
-                h = H[uniq.index(pref[j])]
-                cum, dg = 0, (1 << d) - 1
-                while dg > 0 and cum + int(h[dg]) < need[j]:
-                    cum += int(h[dg])
-                    dg -= 1
-                need[j] -= cum
-                pref[j] = (pref[j] << d) | dg
-            hi -= d
-            if src == 0 and hi > 0:
-                b.sel_compact(sorted(set(pref)), hi)
+        for p in range(passes):
+            h = b.sel_hist(src)
+            c.allreduce_tensor(h)
+            b.sel_pick(h)
+            if p == 0 and passes > 1:
+                b.sel_compact()
                 src = 1
-        return pref, need
 
     def run(self, max_turns=10_000):
         trace = []
@@ -392,7 +375,8 @@ class HipBackend:
         self.h = h
         self.world = world
         # one stream for the engine's kernels and the collectives: ordered without host syncs
-        self.stream = torch.cuda.current_stream(self.device)
+        self.stream = torch.cuda.Stream(self.device)
+        torch.cuda.set_stream(self.stream)
         L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
 
     def _bind(self):
@@ -407,16 +391,18 @@ class HipBackend:
         lib.sbd_owner_claim.argtypes = [vp, vp, vp, i64, vp]
         lib.sbd_apply.argtypes = [vp, vp, p64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
-        lib.sbd_eq_count.argtypes = [vp, u64, p64]
         lib.sbd_key_range.argtypes = [vp, vp]
-        lib.sbd_sel_hist.argtypes = [vp, i32, i32, vp, i32, i32, vp]
-        lib.sbd_sel_compact.argtypes = [vp, i32, vp, i32]
+        lib.sbd_sel_begin.argtypes = [vp, i32, vp, u64, u64]
+        lib.sbd_sel_hist.argtypes = [vp, i32, vp]
+        lib.sbd_sel_pick.argtypes = [vp, vp]
+        lib.sbd_sel_compact.argtypes = [vp]
+        lib.sbd_sel_eq.argtypes = [vp, vp]
         lib.sbd_set_stream.argtypes = [vp, vp]
         lib.sbd_noise_info.argtypes = [vp, vp]
         lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
         lib.sbd_noise_sync.argtypes = [vp]
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
-        lib.sbd_partition.argtypes = [vp, i32, u64, i64, i32, vp, i32, vp]
+        lib.sbd_partition.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
         lib.sbd_pack_kept.argtypes = [vp, vp, vp, vp, vp]
         lib.sbd_receive.argtypes = [vp, vp, vp, vp, vp, i64, i32]
@@ -519,29 +505,31 @@ class HipBackend:
         self._chk(self.lib.sbd_key_range(self.h, out.ctypes.data), 'sbd_key_range')
         return [int(out[0]), int(out[1])]
 
-    def sel_hist(self, src, prefs, hi, d):
-        p = np.ascontiguousarray(np.array(prefs, dtype=np.uint64))
-        out = np.zeros(len(prefs) << d, np.int64)
-        self._chk(self.lib.sbd_sel_hist(self.h, int(src), len(prefs), p.ctypes.data, int(hi), int(d), out.ctypes.data),
-                  'sbd_sel_hist')
-        return out
+    def sel_begin(self, pos, mn, mx):
+        if not hasattr(self, 'sel_h'):
+            self.sel_h = torch.zeros(16 * 1024, dtype=torch.int64, device=self.device)
+            self.sel_eqbuf = torch.zeros(1, dtype=torch.int64, device=self.device)
+        p = np.ascontiguousarray(np.array(pos, dtype=np.int64))
+        self._chk(self.lib.sbd_sel_begin(self.h, len(pos), p.ctypes.data, int(mn), int(mx)), 'sbd_sel_begin')
 
-    def sel_compact(self, prefs, hi):
-        p = np.ascontiguousarray(np.array(prefs, dtype=np.uint64))
-        self._chk(self.lib.sbd_sel_compact(self.h, len(prefs), p.ctypes.data, int(hi)), 'sbd_sel_compact')
+    def sel_hist(self, src):
+        self._chk(self.lib.sbd_sel_hist(self.h, int(src), self.sel_h.data_ptr()), 'sbd_sel_hist')
+        return self.sel_h
 
-    def eq_count(self, T):
-        n = self.C.c_int64()
-        self._chk(self.lib.sbd_eq_count(self.h, int(T), self.C.byref(n)), 'sbd_eq_count')
-        return n.value
+    def sel_pick(self, h):
+        self._chk(self.lib.sbd_sel_pick(self.h, h.data_ptr()), 'sbd_sel_pick')
 
-    def partition(self, top, splits, G):
+    def sel_compact(self):
+        self._chk(self.lib.sbd_sel_compact(self.h), 'sbd_sel_compact')
+
+    def sel_eq(self):
+        self._chk(self.lib.sbd_sel_eq(self.h, self.sel_eqbuf.data_ptr()), 'sbd_sel_eq')
+        return self.sel_eqbuf
+
+    def partition(self, has_top, eq_all, rank, nsplit, G):
         counts = np.zeros(G, np.int64)
-        sp = np.ascontiguousarray(np.asarray(splits, dtype=np.uint64)) if len(splits) else np.zeros(1, np.uint64)
-        has = top is not None
-        T, q = (top if has else (0, 0))
-        self._chk(self.lib.sbd_partition(self.h, int(has), int(T), int(q), len(splits), sp.ctypes.data, int(G),
-                                         counts.ctypes.data), 'sbd_partition')
+        self._chk(self.lib.sbd_partition(self.h, int(bool(has_top)), eq_all.data_ptr() if eq_all is not None else None,
+                                         int(rank), int(nsplit), int(G), counts.ctypes.data), 'sbd_partition')
         self.dest_counts = counts
         return counts
 
