@@ -20,6 +20,9 @@ def main(args):
     from bench import HBM_PEAK_GBS, METRIC, step_bytes
     from splendor_amd.dist import Comm, DistSolve, HipBackend
     from splendor_amd.engine import HEURISTIC_IDS
+    if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
+        os.environ.update(RANK='0', LOCAL_RANK='0', WORLD_SIZE='1', MASTER_ADDR='127.0.0.1',
+                          MASTER_PORT=os.environ.get('MASTER_PORT', '29541'))
     backend = os.environ.get('SB_DIST_BACKEND', 'nccl')
     local = int(os.environ.get('LOCAL_RANK', '0'))
     ndev = torch.cuda.device_count()

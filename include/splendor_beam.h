@@ -169,15 +169,18 @@ int sbd_noise_chunk(sb_engine* e, void* win_out, void* counts_out);   /* device 
 int sbd_noise_sync(sb_engine* e);                                       /* wait for sbd_noise_chunk */
 int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
 
-/* Joint select on the device (dist.py _multiselect): sbd_key_range = min/max of this rank's score keys
- * of the turn; sbd_sel_begin = select state for npos positions (1-based ranks in score-descending
- * order) below the bits common to [kmin, kmax]; per pass: sbd_sel_hist (16 x 1024 int64 histogram of
- * the next 10-bit digit per distinct prefix into hist_dev, over the keys (src 0) or the candidates
- * (src 1)), an all_reduce(SUM) of hist_dev by the caller on the same stream, sbd_sel_pick; after the
- * first pass sbd_sel_compact keeps the keys of the chosen buckets as candidates.  sbd_sel_eq: count of
- * keys equal to position 0's key (int64 at eq_dev) for the all_gather of the keep boundary's ties. */
-int sbd_key_range(sb_engine* e, uint64_t* out2);
-int sbd_sel_begin(sb_engine* e, int32_t npos, const int64_t* positions, uint64_t kmin, uint64_t kmax);
+/* Joint select on the device (dist.py _multiselect), no host round trip: sbd_key_range writes this
+ * rank's score-key range of the turn to range_dev as two int64 for one all_reduce(MIN) by the caller
+ * (kmin ^ 2^63, ~(kmax ^ 2^63)); sbd_sel_begin = select state for npos (<= 15) positions (1-based ranks
+ * in score-descending order) below the bits common to the reduced range; per pass: sbd_sel_hist
+ * (npos x 1024 int64 histogram of the next 10-bit digit per distinct prefix into hist_dev, over the keys
+ * (src 0) or the candidates (src 1)), an all_reduce(SUM) of hist_dev by the caller on the same stream,
+ * sbd_sel_pick; passes after the last digit are no-ops, so the caller runs a fixed 7 (ceil(64/10)).
+ * After the first pass sbd_sel_compact keeps the keys of the chosen buckets as candidates.
+ * sbd_sel_eq: count of keys equal to position 0's key (int64 at eq_dev) for the all_gather of the
+ * keep boundary's ties. */
+int sbd_key_range(sb_engine* e, void* range_dev);
+int sbd_sel_begin(sb_engine* e, int32_t npos, const int64_t* positions, const void* range_dev);
 int sbd_sel_hist(sb_engine* e, int32_t src, void* hist_dev);
 int sbd_sel_pick(sb_engine* e, const void* hist_dev);
 int sbd_sel_compact(sb_engine* e);
@@ -188,11 +191,11 @@ int sbd_sel_eq(sb_engine* e, void* eq_dev);
 int sbd_partition(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t nsplit, int32_t world,
                   int64_t* dest_counts);
 int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, int64_t* dest_counts);
-/* kept records grouped by destination, next_queue order inside a group */
-int sbd_pack_kept(sb_engine* e, uint64_t* d_lo, uint64_t* d_hi, uint64_t* d_par, uint64_t* d_key);
-/* the new slice: received records (global next_queue order), stable-sorted by score if heur */
-int sbd_receive(sb_engine* e, const uint64_t* d_lo, const uint64_t* d_hi, const uint64_t* d_par,
-                const uint64_t* d_key, int64_t n, int32_t heur);
+/* kept records grouped by destination, next_queue order inside a group: 4 x u64 per record
+ * (state lo, state hi, global parent rank, score key), one all_to_all buffer */
+int sbd_pack_kept(sb_engine* e, uint64_t* d_rec);
+/* the new slice: n received 4-word records (global next_queue order), stable-sorted by score if heur */
+int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);
 int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
 
 /* ---- realistic multi-player mode (MultiPlayerState, src/solver.py:471-860; config C4) ----

@@ -889,6 +889,8 @@ struct Engine {
     DBuf<unsigned long long> own_lost;
     DBuf<uint64_t> dsel, dsel_c;          // joint select: prefixes / histograms, candidate keys
     DBuf<uint32_t> dsel_t;                // joint select: compaction tile offsets
+    int dsel_npos = 1;                    // joint select: positions (histogram rows)
+    DBuf<uint64_t> rkey;                  // sharded receive: keys of the received records
     DBuf<uint8_t> digit;
 };
 
@@ -1452,6 +1454,7 @@ void sb_destroy(sb_engine* h) {
     E.dsel.release();
     E.dsel_c.release();
     E.dsel_t.release();
+    E.rkey.release();
     E.part_hist.release();
     E.digit.release();
     if (E.d_tables) (void)hipFree(E.d_tables);

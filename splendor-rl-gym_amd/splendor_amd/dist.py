@@ -5,22 +5,24 @@ positions [off_r, off_r + n_r)), so the (parent rank, ordinal) order that decide
 (src/solver.py:446-450) and the noise order (sorted() calls its key in next_queue order,
 src/solver.py:452-456) stay global.  One step, per rank:
 
-  goal      local first rank per pts -> global (+off) -> all_reduce(MIN)  (src/solver.py:438-445)
+  turn sync one all_gather per turn of (slice size, first local position per pts): slice offsets and
+            the goal check (src/solver.py:438-445)
   expand    every successor of the local parents becomes a record (key, owner = mix64(key) top bits
-            mod world), grouped by owner in (parent, ordinal) order
+            mod world), grouped by owner in (parent, ordinal) order; one all_gather of the per-owner
+            counts sizes the exchange
   dedup     all_to_all of the keys to their owners; records arrive source rank by source rank, so
             the record index at the owner is the global (parent rank, ordinal) order: the owner's
             shard of the global visited set claims with tag = turn | record index and answers one
             byte per record (first occurrence or not); all_to_all back
   offsets   all_gather of per-rank unique counts -> this rank's next_queue offset k_off
-  emit      survivors' states + scores; noise = accepted MT draw (consumed + k_off + k): every rank
-            runs the same jump-ahead MT19937 stream
-  select    top-W of all scores, stable (score desc, next_queue order asc): MSB radix select with
-            all_reduce(SUM) of 256-bin histograms per pass, for the keep boundary and for the
-            world-1 split boundaries of the kept set; ties at the keep boundary are taken in
-            global order via all_gather of per-rank tie counts
-  rebalance all_to_all of the kept records to their destination range; the receiver stable-sorts
-            by score (records arrive in source order = global next_queue order)
+  emit      survivors' states + scores; noise = accepted MT draw (consumed + k_off + k), from the
+            sharded MT19937 stream (ShardNoise)
+  select    top-W of all scores, stable (score desc, next_queue order asc), on the device: MSB radix
+            select with all_reduce(SUM) of 1024-bin histograms per distinct prefix per pass, for the
+            keep boundary and the world-1 split boundaries of the kept set; ties at the keep
+            boundary are taken in global order via all_gather of per-rank tie counts
+  rebalance all_to_all of the kept 32-byte records to their destination range; the receiver
+            stable-sorts by score (records arrive in source order = global next_queue order)
 
 The backend supplies the per-rank compute (HipBackend: libsplendor_beam.so; tests: a Python
 reference backend).  All results are bit-identical to the single-GPU engine and the oracle.
@@ -75,18 +77,18 @@ class Comm:
 
     def alltoall(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
         s = self._to(send)
-        r = torch.empty(int(sum(recv_counts)), dtype=send.dtype, device=s.device)
+        r = torch.empty((int(sum(recv_counts)),) + tuple(send.shape[1:]), dtype=send.dtype, device=s.device)
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
-    def allreduce_tensor(self, t: torch.Tensor):
-        """In-place SUM over ranks of a tensor on this rank's device."""
+    def allreduce_tensor(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
+        """In-place reduction over ranks of a tensor on this rank's device (no host wait with RCCL)."""
         if self.cpu_coll:
             x = t.cpu()
-            dist.all_reduce(x)
+            dist.all_reduce(x, op=op)
             t.copy_(x.to(t.device))
         else:
-            dist.all_reduce(t)
+            dist.all_reduce(t, op=op)
 
     def allgather_array(self, arr: np.ndarray) -> np.ndarray:
         """(world, len) int64 array of every rank's equal-length int vector."""
@@ -186,7 +188,8 @@ class DistSolve:
         self.done = False
         self.max_pts = 0
         self.winner = None                      # (turn, global rank)
-        self.counts = [comm.allgather_int(backend.n_local())]   # per turn: per-rank slice sizes
+        self.counts = []                        # per turn: per-rank slice sizes
+        self._turn_sync()
         self.noise = ShardNoise(backend, comm) if use_heuristic else None
         self.consumed = 0                       # accepted draws used so far (global)
 
@@ -195,11 +198,19 @@ class DistSolve:
         return int(cnt[:self.c.rank].sum())
 
     # ------------------------------------------------------------ goal check (src/solver.py:438-445)
+    def _turn_sync(self):
+        """Once per turn, one all_gather: every rank's slice size and its first local position per
+        pts value, giving the slice offsets and the global first position per pts."""
+        gt = self.b.goal_table().astype(np.int64)
+        M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt]))
+        cnt = M[:, 0].copy()
+        offs = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+        first = M[:, 1:]
+        self.counts.append(cnt)
+        self._goal_g = np.where(first != NONE32, first + offs[:, None], BIG).min(axis=0)
+
     def _goal_check(self, st):
-        first = self.b.goal_table().astype(np.int64)
-        off = self.offset()
-        g = np.where(first != NONE32, first + off, BIG)
-        g = self.c.allreduce(g, dist.ReduceOp.MIN)
+        g = self._goal_g
         win = -1
         for p in range(max(self.goal, 0), 256):
             if g[p] < BIG and (win < 0 or g[p] < win):
@@ -243,11 +254,12 @@ class DistSolve:
         off = self.offset()
         # local expansion + local filter; candidate records grouped by owner
         owner_counts, n_raw = b.expand(off, self.turn, c.world)
-        st['n_raw'] = int(c.allreduce(np.array([n_raw]), dist.ReduceOp.SUM)[0])
+        M = c.allgather_array(np.concatenate([owner_counts, [n_raw]]))   # counts matrix + raw totals
+        st['n_raw'] = int(M[:, -1].sum())
+        recv_counts = M[:, c.rank].copy()
         self._mark(st, 'expand')
         send_key = b.pack()
         self._mark(st, 'pack')
-        recv_counts = c.alltoall_counts(owner_counts)
         rkey = c.alltoall(send_key, owner_counts, recv_counts)
         self._mark(st, 'a2a_keys')
         ret = b.owner_claim(rkey, self.turn)
@@ -286,39 +298,37 @@ class DistSolve:
         else:
             dest_counts = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
-        lo, hi, par, key = b.pack_kept()
+        rec = b.pack_kept()
         self._mark(st, 'pack_kept')
         recv = c.alltoall_counts(dest_counts)
-        rlo = c.alltoall(lo, dest_counts, recv)
-        rhi = c.alltoall(hi, dest_counts, recv)
-        rpar = c.alltoall(par, dest_counts, recv)
-        rkey = c.alltoall(key, dest_counts, recv)
+        rrec = c.alltoall(rec, dest_counts, recv)
         self._mark(st, 'a2a_kept')
-        b.receive(rlo, rhi, rpar, rkey, self.heur)
-        self.counts.append(c.allgather_int(b.n_local()))
+        b.receive(rrec, self.heur)
+        self._turn_sync()
         self._mark(st, 'rebalance')
         self.turn += 1
         st['n_kept'] = int(self.counts[-1].sum())
         return st
 
+    SEL_PASSES = 7   # ceil(64 / 10): passes after the last digit are no-ops on the device
+
     def _multiselect(self, positions, st=None):
         """Global key at each 1-based position of the (score desc) order and how many of its ties
         precede the position, left in the backend's select state: MSB radix select over 10-bit
-        digits below the bits common to every key (global min/max); per pass a histogram per
-        distinct prefix, all_reduce(SUM) on the device, a pick kernel; after the first pass each
-        rank keeps only its keys in the chosen buckets.  The passes are enqueued without waiting."""
+        digits below the bits common to every key (all_reduce(MIN) of the encoded range); per pass
+        a histogram per distinct prefix, all_reduce(SUM) on the device, a pick kernel; after the
+        first pass each rank keeps only its keys in the chosen buckets.  Nothing here waits on the
+        host: the passes and collectives are enqueued on the engine's stream."""
         c, b = self.c, self.b
-        rng = c.allgather_array(np.array([_u64_to_i64(x) for x in b.key_range()], dtype=np.int64))
-        mn = min(x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 0].tolist())
-        mx = max(x & 0xFFFFFFFFFFFFFFFF for x in rng[:, 1].tolist())
-        b.sel_begin(positions, mn, mx)
-        passes = -(-(mn ^ mx).bit_length() // 10)
+        rng = b.key_range()
+        c.allreduce_tensor(rng, dist.ReduceOp.MIN)
+        b.sel_begin(positions, rng)
         src = 0
-        for p in range(passes):
+        for p in range(self.SEL_PASSES):
             h = b.sel_hist(src)
             c.allreduce_tensor(h)
             b.sel_pick(h)
-            if p == 0 and passes > 1:
+            if p == 0:
                 b.sel_compact()
                 src = 1
 
@@ -392,7 +402,7 @@ class HipBackend:
         lib.sbd_apply.argtypes = [vp, vp, p64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_key_range.argtypes = [vp, vp]
-        lib.sbd_sel_begin.argtypes = [vp, i32, vp, u64, u64]
+        lib.sbd_sel_begin.argtypes = [vp, i32, vp, vp]
         lib.sbd_sel_hist.argtypes = [vp, i32, vp]
         lib.sbd_sel_pick.argtypes = [vp, vp]
         lib.sbd_sel_compact.argtypes = [vp]
@@ -404,8 +414,8 @@ class HipBackend:
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
         lib.sbd_partition.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
-        lib.sbd_pack_kept.argtypes = [vp, vp, vp, vp, vp]
-        lib.sbd_receive.argtypes = [vp, vp, vp, vp, vp, i64, i32]
+        lib.sbd_pack_kept.argtypes = [vp, vp]
+        lib.sbd_receive.argtypes = [vp, vp, i64, i32]
         lib.sbd_mark_done.argtypes = [vp, i64]
         lib._sbd_bound = True
 
@@ -501,16 +511,16 @@ class HipBackend:
         self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')
 
     def key_range(self):
-        out = np.zeros(2, np.uint64)
-        self._chk(self.lib.sbd_key_range(self.h, out.ctypes.data), 'sbd_key_range')
-        return [int(out[0]), int(out[1])]
+        rng = torch.empty(2, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_key_range(self.h, rng.data_ptr()), 'sbd_key_range')
+        return rng
 
-    def sel_begin(self, pos, mn, mx):
-        if not hasattr(self, 'sel_h'):
-            self.sel_h = torch.zeros(16 * 1024, dtype=torch.int64, device=self.device)
+    def sel_begin(self, pos, rng):
+        if getattr(self, 'sel_h', None) is None or self.sel_h.numel() != len(pos) * 1024:
+            self.sel_h = torch.zeros(len(pos) * 1024, dtype=torch.int64, device=self.device)
             self.sel_eqbuf = torch.zeros(1, dtype=torch.int64, device=self.device)
         p = np.ascontiguousarray(np.array(pos, dtype=np.int64))
-        self._chk(self.lib.sbd_sel_begin(self.h, len(pos), p.ctypes.data, int(mn), int(mx)), 'sbd_sel_begin')
+        self._chk(self.lib.sbd_sel_begin(self.h, len(pos), p.ctypes.data, rng.data_ptr()), 'sbd_sel_begin')
 
     def sel_hist(self, src):
         self._chk(self.lib.sbd_sel_hist(self.h, int(src), self.sel_h.data_ptr()), 'sbd_sel_hist')
@@ -542,11 +552,10 @@ class HipBackend:
 
     def pack_kept(self):
         n = int(self.dest_counts.sum())
-        lo, hi, par, key = self._empty(n), self._empty(n), self._empty(n), self._empty(n)
-        self._chk(self.lib.sbd_pack_kept(self.h, lo.data_ptr(), hi.data_ptr(), par.data_ptr(), key.data_ptr()),
-                  'sbd_pack_kept')
-        return lo, hi, par, key
+        rec = torch.empty((n, 4), dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n else None), 'sbd_pack_kept')
+        return rec
 
-    def receive(self, lo, hi, par, key, heur):
-        self._chk(self.lib.sbd_receive(self.h, lo.data_ptr(), hi.data_ptr(), par.data_ptr(), key.data_ptr(),
-                                       lo.numel(), int(bool(heur))), 'sbd_receive')
+    def receive(self, rec, heur):
+        self._chk(self.lib.sbd_receive(self.h, rec.data_ptr() if rec.numel() else None, rec.shape[0], int(bool(heur))),
+                  'sbd_receive')
