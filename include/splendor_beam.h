@@ -154,20 +154,25 @@ int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, const uint64_t* d_tag, 
 int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
 /* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */
 int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
-/* Sharded noise stream (world > 1, heuristic): rank r owns MT19937 chunks c = r (mod world), each
- * P producer segments of twists*624 words.  sbd_noise_info: [P, twists, accepted values in the lead
- * block, consumed].  sbd_noise_chunk: the P windows (624 u32 each, device buffer win_out) of the
- * rank's next owned chunk and its per-producer accepted counts (P u32, device buffer counts_out),
- * launched asynchronously (sbd_noise_sync waits).  sbd_noise_fill: regenerate
- * nseg producer segments (device window addresses, global index of each one's first accepted draw)
- * and store the accepted values with global index in [a, b) for this rank's emission. */
+/* Sharded noise stream (heuristic, sharded mode): rank r generates MT19937 chunks c = r (mod world),
+ * each P producer segments of `twists` twists, in count-only mode with a checkpoint every ck twists.
+ * sbd_noise_info: [P, twists, accepted values in the lead block, consumed, ck, S = twists/ck sub-segments
+ * per producer, checkpoint slots, 0].  sbd_noise_chunk: the rank's next owned chunk into checkpoint slot
+ * `slot` (windows kept on this device) and its accepted count per sub-segment (P x S u32, producer-major,
+ * device buffer counts_out), launched asynchronously after the stream's earlier work (sbd_noise_sync
+ * waits).  sbd_noise_pack: copy m checkpoint windows (index = slot * P * S + sub-segment) into wins_out
+ * (m x 624 u32) for the all_to_all to the ranks that consume them.  sbd_noise_fill: regenerate m
+ * sub-segments from contiguous windows (acc0 = global index of each one's first accepted draw) and keep
+ * the accepted values with global index in [a, b) for this rank's emission. */
 /* Run the engine's step work on the caller's stream (e.g. torch.cuda.current_stream(), which the RCCL
  * collectives use): exchanges and kernels are then ordered without host synchronisation. */
 int sbd_set_stream(sb_engine* e, void* stream);
-int sbd_noise_info(sb_engine* e, uint64_t* out4);
-int sbd_noise_chunk(sb_engine* e, void* win_out, void* counts_out);   /* device buffers; asynchronous */
-int sbd_noise_sync(sb_engine* e);                                       /* wait for sbd_noise_chunk */
-int sbd_noise_fill(sb_engine* e, int32_t nseg, const uint64_t* win_ptrs, const uint64_t* acc0, uint64_t a, uint64_t b);
+
+int sbd_noise_info(sb_engine* e, uint64_t* out8);
+int sbd_noise_chunk(sb_engine* e, int32_t slot, void* counts_out);          /* device buffer; asynchronous */
+int sbd_noise_sync(sb_engine* e);                                          /* wait for sbd_noise_chunk */
+int sbd_noise_pack(sb_engine* e, int32_t m, const int64_t* idx, void* wins_out);
+int sbd_noise_fill(sb_engine* e, int32_t m, const void* wins, const uint64_t* acc0, uint64_t a, uint64_t b);
 
 /* Joint select on the device (dist.py _multiselect), no host round trip: sbd_key_range writes this
  * rank's score-key range of the turn to range_dev as two int64 for one all_reduce(MIN) by the caller

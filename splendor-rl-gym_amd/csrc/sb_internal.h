@@ -150,7 +150,11 @@ struct NoiseStream {
     hipEvent_t ev_ready = nullptr;
     bool pending = false;
     bool sharded = false;          // world > 1: values come from noise_shard_fill
-    DBuf<uint64_t> segtab;         // sharded fill: segment windows + first accepted indices
+    DBuf<uint64_t> segtab;         // sharded fill: first accepted index of every window
+    int ck = 1;                    // sharded: twists per checkpoint (sub-segment)
+    int nslots = 4;                // sharded: chunk slots of checkpoint windows
+    DBuf<uint32_t> ckpt;           // sharded: nslots x P x (twists / ck) windows of 624 words
+    hipEvent_t ev_main = nullptr;  // sharded: main-stream point a new chunk waits for (slot reuse)
 };
 void noise_init(NoiseStream& ns, const uint32_t* state625, uint64_t ring_cap_pow2, int64_t twists, hipStream_t st);
 uint64_t noise_chunk_words(const NoiseStream& ns);
@@ -165,8 +169,13 @@ void noise_free(NoiseStream& ns);
 // writes its per-producer accepted counts to d_counts (asynchronously on st); fill() regenerates
 // producer segments into the ring.
 void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st);
-void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* d_counts, hipStream_t st);
-void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+// next owned chunk into checkpoint slot `slot`: per sub-segment (ck twists) accepted counts to d_counts
+// (P x S, producer-major) and the window at its start to the slot; on st_mt after st_main's pending work
+void noise_shard_chunk(NoiseStream& ns, int slot, uint32_t* d_counts, hipStream_t st_main, hipStream_t st_mt);
+// gather checkpoint windows (index = slot * P * S + sub-segment) into d_out (m x 624)
+void noise_shard_pack(NoiseStream& ns, int m, const int64_t* h_idx, uint32_t* d_out, hipStream_t st);
+// regenerate m sub-segments from contiguous windows; accepted values with global index in [a, b) go to the ring
+void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, uint64_t a, uint64_t b,
                       hipStream_t st);
 void noise_mt_state(NoiseStream& ns, uint32_t* out625);
 // debug: raw device words from P producers of `twists` twists per segment

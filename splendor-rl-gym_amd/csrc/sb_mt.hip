@@ -13,7 +13,10 @@
 //   compaction  each producer writes only its accepted draws (in order) to a staging segment
 //               (ballot + wave-count scan per twist); k_mt_place copies the segments into a ring of u8
 //               values, so next_queue element k reads ring[(consumed + k) & mask].
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <vector>
 
@@ -93,11 +96,12 @@ __global__ __launch_bounds__(MT_NT) void k_mt_write(const uint32_t* __restrict__
 // P producers, one workgroup each; producer b runs `twists` twists from window b.  MODE 0 (raw) writes
 // the tempered words (debug); MODE 1 (compact) writes only the accepted randint values (1..100) of
 // the segment, in order, to stage[b * L ..] and their count to counts[b] (fused accept compaction);
-// MODE 2 (count) only counts them (sharded streams, see noise_shard_chunk).
+// MODE 2 (count) only counts them; MODE 3 (checkpoint) counts per sub-segment of ck twists and saves
+// the window at the start of each sub-segment to out (sharded streams, see noise_shard_chunk).
 template <int MODE>
 __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
                                                      uint8_t* __restrict__ stage, uint32_t* __restrict__ counts,
-                                                     int64_t twists) {
+                                                     int64_t twists, int ck = 1) {
     constexpr bool RAW = MODE == 0;
     __shared__ uint32_t buf[2][624];
     __shared__ uint32_t wc[10];
@@ -109,9 +113,15 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
     uint8_t* sg = RAW ? nullptr : stage + b * twists * 624;
     uint32_t run = 0;
     int cur = 0;
+    const int64_t nsub = MODE == 3 ? twists / ck : 0;
     for (int64_t w = 0; w < twists; w++) {
         uint32_t* A = buf[cur];
         uint32_t* B = buf[cur ^ 1];
+        if (MODE == 3 && w % ck == 0) {   // sub-segment boundary: its window, the previous one's count
+            if (t < 624) out[(b * nsub + w / ck) * 624 + t] = A[t];
+            if (t == 0 && w > 0) counts[b * nsub + w / ck - 1] = run;
+            run = 0;
+        }
         if (t < 227) B[t] = mt_mix(A[t], A[t + 1], A[t + 397]);
         __syncthreads();
         if (t < 227) B[227 + t] = mt_mix(A[227 + t], A[228 + t], B[t]);
@@ -139,7 +149,7 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
         }
         cur ^= 1;
     }
-    if (!RAW && t == 0) counts[b] = run;
+    if (!RAW && t == 0) counts[MODE == 3 ? b * nsub + nsub - 1 : b] = run;
 }
 
 // copy each producer's accepted values to the ring at produced + exclusive offset
@@ -157,16 +167,16 @@ __global__ __launch_bounds__(256) void k_mt_place(const uint8_t* __restrict__ st
     for (uint32_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) ring[(base + j) & ring_mask] = src[j];
 }
 
-// Sharded streams: block j regenerates one producer segment from its window seg_win[j] (device
-// address of 624 words); its first accepted draw has global index seg_acc0[j].  Accepted values
-// with global index in [a, b) go to ring[index & ring_mask]; the block stops once past b.
-__global__ __launch_bounds__(640) void k_mt_fill(const uint64_t* __restrict__ seg_win, const uint64_t* __restrict__ seg_acc0,
+// Sharded streams: block j regenerates one sub-segment (twists twists) from window j of wins (624
+// words each); its first accepted draw has global index seg_acc0[j].  Accepted values with global
+// index in [a, b) go to ring[index & ring_mask]; the block stops once past b.
+__global__ __launch_bounds__(640) void k_mt_fill(const uint32_t* __restrict__ wins, const uint64_t* __restrict__ seg_acc0,
                                                   int64_t twists, uint64_t a, uint64_t b, uint8_t* __restrict__ ring,
                                                   uint64_t ring_mask) {
     __shared__ uint32_t buf[2][624];
     __shared__ uint32_t wc[10];
     const int t = threadIdx.x, wv = t >> 6;
-    const uint32_t* win = reinterpret_cast<const uint32_t*>(seg_win[blockIdx.x]);
+    const uint32_t* win = wins + (int64_t)blockIdx.x * 624;
     if (t < 624) buf[0][t] = win[t];
     __syncthreads();
     uint64_t run = seg_acc0[blockIdx.x];
@@ -396,35 +406,64 @@ void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st) {
     SB_HIP(hipMemcpyAsync(pr.stride_poly, w.data(), 624 * 4, hipMemcpyHostToDevice, st));
     SB_HIP(hipStreamSynchronize(st));
     pr.chunk = 0;
+    ns.ck = (int)std::min<int64_t>(pr.twists, 64);   // fill granularity: 64 twists (~31k draws)
+    if (const char* e = getenv("SB_NOISE_CK")) {      // test knob: finer checkpoints (power of two)
+        const int v = atoi(e);
+        if (v >= 1 && v <= ns.ck && !(v & (v - 1))) ns.ck = v;
+    }
     ns.sharded = true;
 }
 
-void noise_shard_chunk(NoiseStream& ns, uint32_t* d_win_out, uint32_t* d_counts, hipStream_t st) {
+void noise_shard_chunk(NoiseStream& ns, int slot, uint32_t* d_counts, hipStream_t st_main, hipStream_t st_mt) {
     MTProducers& pr = ns.prod;
+    if (slot < 0 || slot >= ns.nslots) throw HipError{hipErrorInvalidValue, "noise chunk slot out of range"};
+    const int64_t S = pr.twists / ns.ck;
+    ns.ckpt.ensure((size_t)ns.nslots * pr.P * S * 624);
+    if (!ns.ev_main) SB_HIP(hipEventCreateWithFlags(&ns.ev_main, hipEventDisableTiming));
+    SB_HIP(hipEventRecord(ns.ev_main, st_main));   // earlier packs may still read the slot
+    SB_HIP(hipStreamWaitEvent(st_mt, ns.ev_main, 0));
     if (pr.chunk > 0)
-        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
-    SB_HIP(hipMemcpyAsync(d_win_out, pr.d_win, (size_t)pr.P * 624 * 4, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_mt_gen_par<2>, dim3(pr.P), dim3(640), 0, st, pr.d_win, (uint32_t*)nullptr, (uint8_t*)nullptr,
-                       d_counts, pr.twists);
+        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st_mt, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
+    hipLaunchKernelGGL(k_mt_gen_par<3>, dim3(pr.P), dim3(640), 0, st_mt, pr.d_win,
+                       ns.ckpt.p + (size_t)slot * pr.P * S * 624, (uint8_t*)nullptr, d_counts, pr.twists, ns.ck);
     SB_HIP(hipGetLastError());
-    pr.chunk++;   // asynchronous: the caller synchronises st before using d_win_out / d_counts
+    pr.chunk++;   // asynchronous: the caller synchronises st_mt before using d_counts or the slot
 }
 
-void noise_shard_fill(NoiseStream& ns, int nseg, const uint64_t* h_win, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+__global__ void k_mt_pack(const uint32_t* __restrict__ ckpt, const int64_t* __restrict__ idx, uint32_t* __restrict__ out) {
+    const int64_t j = blockIdx.x;
+    const uint32_t* src = ckpt + idx[j] * 624;
+    for (int t = threadIdx.x; t < 624; t += blockDim.x) out[j * 624 + t] = src[t];
+}
+
+void noise_shard_pack(NoiseStream& ns, int m, const int64_t* h_idx, uint32_t* d_out, hipStream_t st) {
+    if (m <= 0) return;
+    const int64_t lim = (int64_t)ns.nslots * ns.prod.P * (ns.prod.twists / ns.ck);
+    for (int j = 0; j < m; j++)
+        if (h_idx[j] < 0 || h_idx[j] >= lim) throw HipError{hipErrorInvalidValue, "noise window index out of range"};
+    ns.segtab.ensure((size_t)m);
+    SB_HIP(hipMemcpyAsync(ns.segtab.p, h_idx, (size_t)m * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_mt_pack, dim3(m), dim3(256), 0, st, ns.ckpt.p, (const int64_t*)ns.segtab.p, d_out);
+    SB_HIP(hipGetLastError());   // (pageable-source copy above completes before returning)
+}
+
+void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, uint64_t a, uint64_t b,
                       hipStream_t st) {
-    if (nseg <= 0 || a >= b) return;
-    ns.segtab.ensure((size_t)nseg * 2);
-    SB_HIP(hipMemcpyAsync(ns.segtab.p, h_win, (size_t)nseg * 8, hipMemcpyHostToDevice, st));
-    SB_HIP(hipMemcpyAsync(ns.segtab.p + nseg, h_acc0, (size_t)nseg * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_mt_fill, dim3(nseg), dim3(640), 0, st, ns.segtab.p, ns.segtab.p + nseg, ns.prod.twists, a, b,
-                       ns.ring.p, ns.ring_mask);
-    SB_HIP(hipGetLastError());   // (pageable-source copies above complete before returning)
+    if (m <= 0 || a >= b) return;
+    ns.segtab.ensure((size_t)m);
+    SB_HIP(hipMemcpyAsync(ns.segtab.p, h_acc0, (size_t)m * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_mt_fill, dim3(m), dim3(640), 0, st, d_wins, ns.segtab.p, (int64_t)ns.ck, a, b, ns.ring.p,
+                       ns.ring_mask);
+    SB_HIP(hipGetLastError());
 }
 
 void noise_free(NoiseStream& ns) {
     if (ns.d_total) (void)hipFree(ns.d_total);
     if (ns.h_total) (void)hipHostFree(ns.h_total);
     if (ns.ev_ready) (void)hipEventDestroy(ns.ev_ready);
+    if (ns.ev_main) (void)hipEventDestroy(ns.ev_main);
+    ns.ev_main = nullptr;
+    ns.ckpt.release();
     ns.prod.release();
     ns.segtab.release();
     ns.raw.release();

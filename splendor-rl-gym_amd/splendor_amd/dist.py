@@ -123,56 +123,83 @@ class ShardNoise:
     The k-th next_queue entry scores with the k-th accepted MT19937 draw (src/solver.py:452-456);
     rank r emits entries [k_off, k_off + n_loc) of each turn.  The raw stream after the lead block is
     cut into chunks of P producer segments; rank r generates chunks c = r (mod world) in count-only
-    mode, every rank all-gathers the per-producer accepted counts and start windows, and each rank
-    regenerates just the producer segments that cover its own window.  Per step a rank generates
-    about 2/world of the stream instead of all of it.
+    mode, keeping a checkpoint window every ck twists (a sub-segment) on its device, and every rank
+    all-gathers the per-sub-segment accepted counts.  Once the turn's offsets are known every rank
+    knows every rank's draw range, so the generating ranks send the windows of the sub-segments each
+    rank needs in one all_to_all (sizes computed identically everywhere, no request round), and each
+    rank regenerates just those sub-segments.  Per step a rank generates about 2/world of the stream.
     """
 
     def __init__(self, backend, comm: Comm):
         self.b, self.c = backend, comm
         info = backend.noise_info()
-        self.P = int(info[0])
+        self.P, self.S, self.nslots = int(info[0]), int(info[5]), int(info[6])
         self.gen_total = int(info[2])   # accepted draws available (global index), the lead block first
-        self.chunks = []                # (first global accepted index, cumulative counts (P+1), windows)
-        self.pending = None             # (counts, windows) of a round launched but not yet gathered
+        self.round = 0                  # chunk rounds launched (one chunk per rank each)
+        self.chunks = []                # (first global accepted index, cumulative counts (P*S+1), rank, slot)
+        self.pending = None             # (slot, counts) of a round launched but not yet gathered
+
+    def _launch(self):
+        slot = self.round % self.nslots
+        if any(ch[3] == slot for ch in self.chunks):
+            raise RuntimeError('noise checkpoint slot still holds unconsumed draws')
+        self.pending = (slot, self.b.noise_chunk(slot))
+        self.round += 1
 
     def _collect(self):
-        """All-gather the round launched by noise_chunk (every rank one chunk)."""
+        """All-gather the sub-segment counts of the round launched by _launch (every rank one chunk)."""
         c, b = self.c, self.b
-        counts, win = self.pending
+        slot, counts = self.pending
         self.pending = None
         b.noise_sync()
         allc = [x.cpu().numpy().astype(np.int64) for x in c.allgather_tensor(counts)]
-        wins = c.allgather_tensor(win)
         for r in range(c.world):   # chunk order: this round's chunk of rank 0, 1, ...
             cum = np.concatenate([[0], np.cumsum(allc[r])]).astype(np.int64)
-            self.chunks.append((self.gen_total, cum, wins[r]))
+            self.chunks.append((self.gen_total, cum, r, slot))
             self.gen_total += int(cum[-1])
 
-    def prepare(self, A: int, N: int, k_off: int, n_loc: int):
+    @staticmethod
+    def _subsegs(s0, cum, a, e):
+        """Non-empty sub-segments of a chunk holding draws with global index in [a, e)."""
+        if e <= a or s0 + cum[-1] <= a or s0 >= e:
+            return np.zeros(0, np.int64)
+        j0 = max(0, int(np.searchsorted(cum, a - s0, side='right')) - 1)
+        j1 = min(len(cum) - 1, int(np.searchsorted(cum, e - s0, side='left')))
+        js = np.arange(j0, j1, dtype=np.int64)
+        return js[(cum[js + 1] > cum[js]) & (cum[js + 1] > a - s0)]
+
+    def prepare(self, A: int, N: int, all_n: np.ndarray):
         """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission."""
         c, b = self.c, self.b
         if self.pending is not None:
             self._collect()
         while self.gen_total < A + N:
-            self.pending = b.noise_chunk()
+            self._launch()
             self._collect()
-        a, e = A + k_off, A + k_off + n_loc
-        segs = []
-        for s0, cum, win in self.chunks:
-            if s0 + cum[-1] <= a or s0 >= e:
-                continue
-            p0 = max(0, int(np.searchsorted(cum, a - s0, side='right')) - 1)
-            for p in range(p0, self.P):
-                if s0 + cum[p] >= e:
-                    break
-                if cum[p + 1] > cum[p]:
-                    segs.append((win, p, s0 + int(cum[p])))
-        b.noise_fill(segs, a, e)
+        starts = A + np.concatenate([[0], np.cumsum(all_n)]).astype(np.int64)
+        me, PS = c.rank, self.P * self.S
+        send = [[] for _ in range(c.world)]
+        recv = [[] for _ in range(c.world)]
+        for s0, cum, g, slot in self.chunks:
+            for r in range(c.world):
+                if g != me and r != me:
+                    continue
+                js = self._subsegs(s0, cum, int(starts[r]), int(starts[r + 1]))
+                if g == me:
+                    send[r].append(slot * PS + js)
+                if r == me:
+                    recv[g].append(s0 + cum[js])
+        cat = lambda xs: np.concatenate(xs).astype(np.int64) if xs else np.zeros(0, np.int64)
+        send = [cat(x) for x in send]
+        recv = [cat(x) for x in recv]
+        wins = b.noise_pack(cat(send))
+        if c.world > 1:
+            wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv])
+        b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
         # next round in the background (side stream) while the step goes on; gathered next turn
         if self.gen_total < A + N + 2 * N:
-            self.pending = b.noise_chunk()
+            self._launch()
 
 
 class DistSolve:
@@ -277,7 +304,7 @@ class DistSolve:
             st.update(done=True, winner_rank=last)
             return st
         if self.heur:
-            self.noise.prepare(self.consumed, N, k_off, n_loc)
+            self.noise.prepare(self.consumed, N, all_n)
             self.consumed += N
         self._mark(st, 'noise')
         b.emit(k_off, N, off)
@@ -409,8 +436,9 @@ class HipBackend:
         lib.sbd_sel_eq.argtypes = [vp, vp]
         lib.sbd_set_stream.argtypes = [vp, vp]
         lib.sbd_noise_info.argtypes = [vp, vp]
-        lib.sbd_noise_chunk.argtypes = [vp, vp, vp]
+        lib.sbd_noise_chunk.argtypes = [vp, i32, vp]
         lib.sbd_noise_sync.argtypes = [vp]
+        lib.sbd_noise_pack.argtypes = [vp, i32, vp, vp]
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
         lib.sbd_partition.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
@@ -487,25 +515,31 @@ class HipBackend:
         return n.value
 
     def noise_info(self):
-        out = np.zeros(4, np.uint64)
+        out = np.zeros(8, np.uint64)
         self._chk(self.lib.sbd_noise_info(self.h, out.ctypes.data), 'sbd_noise_info')
-        self.P = int(out[0])
+        self.P, self.S = int(out[0]), int(out[5])
         return [int(x) for x in out]
 
-    def noise_chunk(self):
-        win = torch.empty(self.P * 624, dtype=torch.int32, device=self.device)
-        counts = torch.empty(self.P, dtype=torch.int32, device=self.device)
-        self._chk(self.lib.sbd_noise_chunk(self.h, win.data_ptr(), counts.data_ptr()), 'sbd_noise_chunk')
-        return counts, win
+    def noise_chunk(self, slot):
+        counts = torch.empty(self.P * self.S, dtype=torch.int32, device=self.device)
+        self._chk(self.lib.sbd_noise_chunk(self.h, int(slot), counts.data_ptr()), 'sbd_noise_chunk')
+        return counts
 
     def noise_sync(self):
         self._chk(self.lib.sbd_noise_sync(self.h), 'sbd_noise_sync')
 
-    def noise_fill(self, segs, a, e):
-        ptrs = np.array([w.data_ptr() + p * 624 * 4 for w, p, _ in segs], dtype=np.uint64)
-        acc0 = np.array([x for _, _, x in segs], dtype=np.uint64)
-        self._chk(self.lib.sbd_noise_fill(self.h, len(segs), ptrs.ctypes.data if len(segs) else None,
-                                          acc0.ctypes.data if len(segs) else None, int(a), int(e)), 'sbd_noise_fill')
+    def noise_pack(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        wins = torch.empty((len(idx), 624), dtype=torch.int32, device=self.device)
+        if len(idx):
+            self._chk(self.lib.sbd_noise_pack(self.h, len(idx), idx.ctypes.data, wins.data_ptr()), 'sbd_noise_pack')
+        return wins
+
+    def noise_fill(self, wins, acc0, a, e):
+        acc0 = np.ascontiguousarray(acc0, dtype=np.uint64)
+        if len(acc0):
+            self._chk(self.lib.sbd_noise_fill(self.h, len(acc0), wins.data_ptr(), acc0.ctypes.data, int(a), int(e)),
+                      'sbd_noise_fill')
 
     def emit(self, k_off, N, off):
         self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')

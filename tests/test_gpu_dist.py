@@ -28,6 +28,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, cfg, outdir):
+    if 'ck' in cfg:
+        os.environ['SB_NOISE_CK'] = str(cfg['ck'])
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
@@ -64,6 +66,8 @@ CASES = [
     (3, {'goal': 6, 'hid': 0, 'name': 'simple', 'width': 250, 'seed': 2, 'heur': True}),
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True}),
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
+    # 8 twists per producer segment, a checkpoint window every twist: sub-segment windows cross ranks
+    (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1}),
 ]
 
 
