@@ -99,22 +99,26 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
     const uint64_t d = sh < SEL_D ? sh : SEL_D;
     const uint64_t dmask = (1ull << d) - 1;
     const uint64_t lt = lanemask_lt();
-    for (int64_t i0 = (int64_t)blockIdx.x * TK_NT; i0 < n; i0 += (int64_t)gridDim.x * TK_NT) {
-        const int64_t i = i0 + threadIdx.x;
-        int b = -1;
-        if (i < n) {
-            const uint64_t k = keys[i];
-            if (hi_bits(k, sh) == prefix) b = (int)((k >> (sh - d)) & dmask);
-        }
-        // scores cluster: lanes sharing the first active lane's bin add once (wave-aggregated)
-        const uint64_t act = __ballot(b >= 0);
-        if (act) {
-            const int b0 = __shfl(b, __builtin_ctzll(act), 64);
-            const uint64_t same = __ballot(b == b0);
-            if (b == b0) {
-                if ((same & lt) == 0) atomicAdd(&h[w][b0], (uint32_t)__popcll(same));
-            } else if (b >= 0) {
-                atomicAdd(&h[w][b], 1u);
+    constexpr int U = 8;   // loads in flight per thread
+    const int64_t stride = (int64_t)gridDim.x * TK_NT;
+    for (int64_t i0 = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i0 < n; i0 += stride * U) {
+        uint64_t kk[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) kk[u] = i0 + u * stride < n ? keys[i0 + u * stride] : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            int b = -1;
+            if (i0 + u * stride < n && hi_bits(kk[u], sh) == prefix) b = (int)((kk[u] >> (sh - d)) & dmask);
+            // scores cluster: lanes sharing the first active lane's bin add once (wave-aggregated)
+            const uint64_t act = __ballot(b >= 0);
+            if (act) {
+                const int b0 = __shfl(b, __builtin_ctzll(act), 64);
+                const uint64_t same = __ballot(b == b0);
+                if (b == b0) {
+                    if ((same & lt) == 0) atomicAdd(&h[w][b0], (uint32_t)__popcll(same));
+                } else if (b >= 0) {
+                    atomicAdd(&h[w][b], 1u);
+                }
             }
         }
     }
@@ -220,8 +224,10 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
     }
 }
 
-// Order-preserving partition of a tile (striped loads, a workgroup scan per 256-element round):
-// elements above the prefix -> (gk, gi) at *gbase + rank; equal ones -> (ek, ei) at *ebase + rank,
+// Order-preserving partition of a tile (4096 elements, striped: element r*256 + t is thread t's r-th):
+// all 16 keys of a thread are loaded up front; per round and wave a ballot per class; one scan over
+// the tile's 16 x 4 (round, wave) counts orders everything (two barriers per tile).
+// Elements above the prefix -> (gk, gi) at *gbase + rank; equal ones -> (ek, ei) at *ebase + rank,
 // only the first *limit of them if limit is given.
 __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
                                                     int64_t n_host, const uint64_t* __restrict__ n_dev,
@@ -230,40 +236,59 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ gi, const uint64_t* __restrict__ gbase,
                                                     uint64_t* __restrict__ ek, uint32_t* __restrict__ ei,
                                                     const uint64_t* __restrict__ ebase, const uint64_t* __restrict__ limit) {
-    __shared__ uint32_t lds[TK_NT / 64 + 1];
+    constexpr int NW = TK_NT / 64;
+    __shared__ uint32_t cnt[TK_IPT * NW];   // (round, wave): above | equal << 16, then exclusive offsets
     const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
     const int64_t base = (int64_t)blockIdx.x * TK_TILE;
     if (base >= n) return;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
+    uint64_t kk[TK_IPT];
+#pragma unroll
+    for (int r = 0; r < TK_IPT; r++) {
+        const int64_t i = base + (int64_t)r * TK_NT + t;
+        kk[r] = i < n ? keys[i] : 0ull;
+    }
+    uint32_t fg = 0, fe = 0;   // bit r: this thread's r-th element is above / equal
+#pragma unroll
+    for (int r = 0; r < TK_IPT; r++) {
+        const int64_t i = base + (int64_t)r * TK_NT + t;
+        const uint64_t hb = hi_bits(kk[r], sh);
+        const bool g = i < n && hb > prefix, e = i < n && hb == prefix;
+        fg |= (uint32_t)g << r;
+        fe |= (uint32_t)e << r;
+        const uint64_t bg = __ballot(g), be = __ballot(e);
+        if (l == 0) cnt[r * NW + w] = (uint32_t)__popcll(bg) | ((uint32_t)__popcll(be) << 16);
+    }
+    __syncthreads();
+    if (t < 64) {   // exclusive scan of the 64 packed counts (round-major = index order)
+        const uint32_t v = t < TK_IPT * NW ? cnt[t] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (t < TK_IPT * NW) cnt[t] = inc - v;
+    }
+    __syncthreads();
+    if (!(fg | fe)) return;
+    const uint64_t og = (gbase ? *gbase : 0) + gt_off[blockIdx.x];
+    const uint64_t oe = eq_off[blockIdx.x];   // rank among equal elements before this tile
     const uint64_t lim = limit ? *limit : ~0ull;
-    uint64_t og = (gbase ? *gbase : 0) + gt_off[blockIdx.x];
-    uint64_t re = eq_off[blockIdx.x];   // rank among equal elements
     const uint64_t eb = ebase ? *ebase : 0;
-    for (int j = 0; j < TK_IPT; j++) {
-        const int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
-        uint64_t k = 0;
-        uint32_t fg = 0, fe = 0;
-        if (i < n) {
-            k = keys[i];
-            const uint64_t hb = hi_bits(k, sh);
-            fg = hb > prefix;
-            fe = hb == prefix;
-        }
-        uint32_t tg, te;
-        const uint32_t rg = block_excl_scan<TK_NT>(fg, lds, &tg);
-        const uint32_t rv = block_excl_scan<TK_NT>(fe, lds, &te);
-        if (fg || fe) {
-            const uint32_t v = idx ? idx[i] : (uint32_t)i;
-            if (fg) {
-                gk[og + rg] = k;
-                gi[og + rg] = v;
-            } else if (re + rv < lim) {
-                ek[eb + re + rv] = k;
-                ei[eb + re + rv] = v;
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int r = 0; r < TK_IPT; r++) {
+        const uint64_t bg = __ballot((fg >> r) & 1), be = __ballot((fe >> r) & 1);
+        const int64_t i = base + (int64_t)r * TK_NT + t;
+        const uint32_t c = cnt[r * NW + w];
+        if ((fg >> r) & 1) {
+            const uint64_t o = og + (c & 0xFFFFu) + __popcll(bg & lt);
+            gk[o] = kk[r];
+            gi[o] = idx ? idx[i] : (uint32_t)i;
+        } else if ((fe >> r) & 1) {
+            const uint64_t re = oe + (c >> 16) + __popcll(be & lt);
+            if (re < lim) {
+                ek[eb + re] = kk[r];
+                ei[eb + re] = idx ? idx[i] : (uint32_t)i;
             }
         }
-        og += tg;
-        re += te;
     }
 }
 
