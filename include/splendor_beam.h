@@ -138,18 +138,30 @@ int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const
 /* Stable descending sort of n u64 keys: out_idx = permutation (ties keep input order), first `keep`. */
 int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx);
 
-/* ---- sharded mode (cfg.world_size > 1): per-rank step primitives; the exchanges between them are
- * the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers are caller-owned
- * buffers on the engine's device; every call returns after its device work has completed. ---- */
+/* ---- sharded mode (cfg.world_size > 1 or flags bit 1): per-rank step primitives; the exchanges
+ * between them are the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers
+ * are caller-owned buffers on the engine's device.  The engine's work is ordered on its stream
+ * (sbd_set_stream); calls that return host values wait for it. ---- */
 /* local first rank per pts of this rank's queue slice (0xFFFFFFFF = none) */
 int sbd_goal_table(sb_engine* e, uint32_t* first256);
-/* expand the local slice (global queue offset goff), drop children this rank generated before or
- * earlier this turn; owner_counts[world] = records per owner rank, *n_raw = successors generated */
-int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int64_t* owner_counts, int64_t* n_raw);
-/* candidate records grouped by owner (rank, ordinal order inside a group): key, global tag */
+/* expand the local slice (global queue offset goff): every successor becomes a record (key, owner =
+ * fmix64(key) >> 40 mod world), stably partitioned by owner.  The records are cut into nchunk (<= 16)
+ * exchange chunks of whole 4096-record tiles; chunk_owner_counts[nchunk][world] = records per chunk
+ * and owner, *n_raw = successors generated */
+int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int32_t nchunk, int64_t* chunk_owner_counts,
+               int64_t* n_raw);
+/* the record keys grouped by owner, (parent, ordinal) order inside a group (d_tag unused: tags are
+ * implicit in the order) */
 int sbd_pack(sb_engine* e, uint64_t* d_key, uint64_t* d_tag);
-/* owner side: claim n received records in this rank's trail shard; d_ret[i] = 1 if first occurrence */
-int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, const uint64_t* d_tag, int64_t n, uint8_t* d_ret);
+/* owner side, per turn: begin(n_total records this owner receives), one claim per received chunk (in
+ * any order: tags carry the global order), finish.  A chunk holds nseg source segments: source q's
+ * records at [seg_start[q], seg_start[q+1]) (seg_start[0] = 0), global record indices seg_base[q]..
+ * (source rank major, then parent order).  d_ret[global index] = 1 for a first occurrence, final
+ * after sbd_owner_finish. */
+int sbd_owner_begin(sb_engine* e, int64_t n_total);
+int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, int64_t n, int32_t nseg, const int64_t* seg_start,
+                    const int64_t* seg_base, uint8_t* d_ret);
+int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
 /* apply the answers (in pack order); *n_unique_local = this rank's next_queue entries */
 int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
 /* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */

@@ -887,6 +887,7 @@ struct Engine {
     DBuf<uint64_t> cand_key, cand_tag;
     DBuf<uint32_t> cand_ro, cand_pos, own_slot, part_hist;
     DBuf<unsigned long long> own_lost;
+    int64_t own_n = 0;                    // sharded: records claimed at this owner this turn
     DBuf<uint64_t> dsel, dsel_c;          // joint select: prefixes / histograms, candidate keys
     DBuf<uint32_t> dsel_t;                // joint select: compaction tile offsets
     int dsel_npos = 1;                    // joint select: positions (histogram rows)

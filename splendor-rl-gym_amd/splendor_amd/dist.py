@@ -81,6 +81,25 @@ class Comm:
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
+    def alltoall_pieces(self, pieces, recv_sizes):
+        """Start an all_to_all of pieces[o] (views, any layout) to rank o; returns (receive buffer,
+        handle).  RCCL runs it asynchronously on its own stream; wait(handle) orders this rank's stream
+        after it.  gloo (no list all_to_all) packs the pieces and completes at once."""
+        out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=pieces[0].device)
+        if self.cpu_coll:
+            send = torch.cat([p.cpu() for p in pieces])
+            r = torch.empty(int(sum(recv_sizes)), dtype=send.dtype)
+            dist.all_to_all_single(r, send, [int(x) for x in recv_sizes], [int(p.numel()) for p in pieces])
+            out.copy_(r.to(out.device))
+            return out, None
+        outs = list(out.split([int(x) for x in recv_sizes]))
+        return out, dist.all_to_all(outs, list(pieces), async_op=True)
+
+    @staticmethod
+    def wait(handle):
+        if handle is not None:
+            handle.wait()
+
     def allreduce_tensor(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
         """In-place reduction over ranks of a tensor on this rank's device (no host wait with RCCL)."""
         if self.cpu_coll:
@@ -219,6 +238,8 @@ class DistSolve:
         self._turn_sync()
         self.noise = ShardNoise(backend, comm) if use_heuristic else None
         self.consumed = 0                       # accepted draws used so far (global)
+        self.nchunk = int(os.environ.get('SB_DIST_CHUNKS', '4'))   # key exchange / claim pipeline depth
+        self.chunk_min = int(os.environ.get('SB_DIST_CHUNK_MIN', str(1 << 23)))   # fewer raw records: one chunk
 
     def offset(self, turn=None) -> int:
         cnt = self.counts[self.turn if turn is None else turn]
@@ -280,18 +301,39 @@ class DistSolve:
             return st
         off = self.offset()
         # local expansion + local filter; candidate records grouped by owner
-        owner_counts, n_raw = b.expand(off, self.turn, c.world)
-        M = c.allgather_array(np.concatenate([owner_counts, [n_raw]]))   # counts matrix + raw totals
+        # exchange chunks: claims of chunk j overlap the transfer of chunk j+1
+        C = self.nchunk if st['n_parents'] * 24 >= self.chunk_min else 1
+        cc, n_raw = b.expand(off, self.turn, c.world, C)            # (C, world) records per chunk, owner
+        M = c.allgather_array(np.concatenate([cc.ravel(), [n_raw]]))
         st['n_raw'] = int(M[:, -1].sum())
-        recv_counts = M[:, c.rank].copy()
+        Mc = M[:, :-1].reshape(c.world, C, c.world)                 # [source][chunk][owner]
+        me = c.rank
         self._mark(st, 'expand')
         send_key = b.pack()
         self._mark(st, 'pack')
-        rkey = c.alltoall(send_key, owner_counts, recv_counts)
-        self._mark(st, 'a2a_keys')
-        ret = b.owner_claim(rkey, self.turn)
-        self._mark(st, 'claim')
-        back = c.alltoall(ret, recv_counts, owner_counts)
+        mine = Mc[me]                                               # my records per chunk, owner
+        ostart = np.concatenate([[0], np.cumsum(mine.sum(axis=0))])  # owner groups in send_key
+        ochunk = np.concatenate([np.zeros((1, c.world), np.int64), np.cumsum(mine, axis=0)])
+        from_src = Mc[:, :, me]                                     # [source][chunk] records to me
+        src_tot = from_src.sum(axis=1)
+        src_base = np.concatenate([[0], np.cumsum(src_tot)])        # global index base per source
+        src_chunk = np.concatenate([np.zeros((c.world, 1), np.int64), np.cumsum(from_src, axis=1)], axis=1)
+        handles = []
+        for j in range(C):
+            pieces = [send_key[int(ostart[o] + ochunk[j, o]):int(ostart[o] + ochunk[j + 1, o])]
+                      for o in range(c.world)]
+            handles.append(c.alltoall_pieces(pieces, from_src[:, j]))
+        n_own = int(src_tot.sum())
+        b.owner_begin(n_own)
+        ret = b.answer_buffer(n_own)
+        for j, (rkey, hd) in enumerate(handles):
+            c.wait(hd)
+            starts = np.concatenate([[0], np.cumsum(from_src[:, j])[:-1]])
+            bases = src_base[:-1] + src_chunk[:, j]
+            b.owner_claim(rkey, starts, bases, ret)
+        b.owner_finish(ret)
+        self._mark(st, 'a2a_keys+claim')
+        back = c.alltoall(ret, src_tot, ostart[1:] - ostart[:-1])
         n_loc = b.apply(back)
         self._mark(st, 'dedup_exchange')
         all_n = c.allgather_int(n_loc)
@@ -423,9 +465,11 @@ class HipBackend:
         vp, i64, u64, i32 = C.c_void_p, C.c_int64, C.c_uint64, C.c_int32
         p64 = C.POINTER(C.c_int64)
         lib.sbd_goal_table.argtypes = [vp, vp]
-        lib.sbd_expand.argtypes = [vp, i64, i32, vp, p64]
+        lib.sbd_expand.argtypes = [vp, i64, i32, i32, vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
-        lib.sbd_owner_claim.argtypes = [vp, vp, vp, i64, vp]
+        lib.sbd_owner_begin.argtypes = [vp, i64]
+        lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
+        lib.sbd_owner_finish.argtypes = [vp, vp]
         lib.sbd_apply.argtypes = [vp, vp, p64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_key_range.argtypes = [vp, vp]
@@ -486,13 +530,14 @@ class HipBackend:
         return out
 
     # ---------------------------------------------------------------- step primitives
-    def expand(self, off, turn, world):
+    def expand(self, off, turn, world, nchunk=1):
         C = self.C
-        counts = np.zeros(world, np.int64)
+        counts = np.zeros(nchunk * world, np.int64)
         nraw = C.c_int64()
-        self._chk(self.lib.sbd_expand(self.h, int(off), int(world), counts.ctypes.data, C.byref(nraw)), 'sbd_expand')
-        self.owner_counts = counts
-        return counts, nraw.value
+        self._chk(self.lib.sbd_expand(self.h, int(off), int(world), int(nchunk), counts.ctypes.data, C.byref(nraw)),
+                  'sbd_expand')
+        self.owner_counts = counts.reshape(nchunk, world).sum(axis=0)
+        return counts.reshape(nchunk, world), nraw.value
 
     def _empty(self, n, dtype=torch.int64):
         return torch.empty(int(n), dtype=dtype, device=self.device)
@@ -503,11 +548,20 @@ class HipBackend:
         self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), None), 'sbd_pack')
         return key
 
-    def owner_claim(self, rkey, turn):
-        ret = self._empty(rkey.numel(), torch.uint8)
-        self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr(), None, rkey.numel(), ret.data_ptr()),
-                  'sbd_owner_claim')
-        return ret
+    def answer_buffer(self, n):
+        return self._empty(max(int(n), 1), torch.uint8)[:int(n)]
+
+    def owner_begin(self, n_total):
+        self._chk(self.lib.sbd_owner_begin(self.h, int(n_total)), 'sbd_owner_begin')
+
+    def owner_claim(self, rkey, starts, bases, ret):
+        st = np.ascontiguousarray(starts, dtype=np.int64)
+        ba = np.ascontiguousarray(bases, dtype=np.int64)
+        self._chk(self.lib.sbd_owner_claim(self.h, rkey.data_ptr() if rkey.numel() else None, rkey.numel(), len(st),
+                                           st.ctypes.data, ba.ctypes.data, ret.data_ptr()), 'sbd_owner_claim')
+
+    def owner_finish(self, ret):
+        self._chk(self.lib.sbd_owner_finish(self.h, ret.data_ptr()), 'sbd_owner_finish')
 
     def apply(self, back):
         n = self.C.c_int64()

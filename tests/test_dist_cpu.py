@@ -27,6 +27,9 @@ def _free_port():
 
 
 def _worker(rank, world, port, cfg, outdir):
+    if 'chunks' in cfg:
+        os.environ['SB_DIST_CHUNKS'] = str(cfg['chunks'])
+        os.environ['SB_DIST_CHUNK_MIN'] = '0'
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
@@ -65,6 +68,8 @@ CASES = [
     (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True}),
     (2, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 40, 'seed': 3, 'heur': True}),
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
+    # key exchange in 3 chunks (claims in chunk order, displacements across chunks)
+    (2, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'chunks': 3}),
 ]
 
 

@@ -28,6 +28,9 @@ def _free_port():
 
 
 def _worker(rank, world, port, cfg, outdir):
+    if 'chunks' in cfg:
+        os.environ['SB_DIST_CHUNKS'] = str(cfg['chunks'])
+        os.environ['SB_DIST_CHUNK_MIN'] = '0'
     if 'ck' in cfg:
         os.environ['SB_NOISE_CK'] = str(cfg['ck'])
     import sys
@@ -68,6 +71,8 @@ CASES = [
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
     # 8 twists per producer segment, a checkpoint window every twist: sub-segment windows cross ranks
     (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1}),
+    # key exchange in 3 chunks (claims in chunk order, displacements across chunks)
+    (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3}),
 ]
 
 
