@@ -899,6 +899,7 @@ static void check_err_word(Engine& E) {
     uint32_t e = E.h_small[1];
     if (e & 1u) throw HipError{hipErrorOutOfMemory, "visited set overfull (probe limit); raise visited_log2"};
     if (e & 2u) throw HipError{hipErrorInvalidValue, "saved >= 256 exceeds the pow tables"};
+    if (e & 4u) throw HipError{hipErrorLaunchFailure, "top-k sort look-back wait exceeded its bound"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -1092,7 +1093,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     uint32_t* idx = nullptr;
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
-        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true);
+        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true, E.d_small + 1);
         idx = E.kidx.p;
     }
     if (timing) SB_HIP(hipEventRecord(ev[5], E.s));

@@ -97,18 +97,18 @@ struct TopkScratch {
     DBuf<uint32_t> v0, v1;          // payload ping-pong
     DBuf<uint64_t> ck;              // select candidates (keys)
     DBuf<uint32_t> ci;              // select candidates (indices)
-    DBuf<uint32_t> tile_hist;       // 256 x ntiles
+    DBuf<uint64_t> os;              // LSD sort: digit histograms, tickets, look-back granules
     DBuf<uint32_t> tile_a, tile_b;  // partition counts
     DBuf<uint64_t> small;           // select state + histogram
-    ScanScratch scan;
     void release();
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.
 // Returns the number written (min(n, keep)).  ms_select/ms_sort get device times if non-null.
 // range_ready: the producer of the keys already folded their min/max into the pair returned by
-// topk_range_reset (called before it ran on the same stream).
+// topk_range_reset (called before it ran on the same stream).  err (device word): bit 4 is set if the
+// sort's look-back wait hit its spin bound (reported by check_err_word; never expected).
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready = false);
+                         hipStream_t st, bool range_ready = false, uint32_t* err = nullptr);
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st);
 // size the scratch for n keys and keep kept (avoids allocation on the step path)
 void topk_reserve(TopkScratch& s, int64_t n, int64_t keep);

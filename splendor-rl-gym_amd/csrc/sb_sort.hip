@@ -12,8 +12,10 @@
 //      (first in index order) are kept; a final partition appends the candidates above T, then those
 //      ties.  The three output groups have disjoint key sets, so a stable sort of the concatenation
 //      orders ties by index exactly as sorted() does;
-//   5. a stable LSD radix sort (8-bit digits) on ~key orders the kept set; digits above the highest
-//      bit that differs inside [lowest kept key, max] are constant and skipped on the device.
+//   5. a stable LSD radix sort (8-bit digits) on ~key orders the kept set, one kernel per digit with
+//      decoupled look-back; digits above the highest bit that differs inside [lowest kept key, max]
+//      are constant and skipped on the device.  (Measured on 4M keys, profiles/sortbench.py: 47 us
+//      per pass, 35 of them without the look-back wait; 90 us for the histograms of all digits.)
 #include <algorithm>
 
 #include "sb_block.h"
@@ -307,76 +309,190 @@ __global__ void k_tk_sortsetup(uint64_t* st, int selected) {
     st[ST_TOPK] = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
 }
 
-__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] + 7) / 8); }
+// ---- stable LSD radix sort of the kept set, one kernel per 8-bit digit (decoupled look-back)
+// Digit p of key k is (~k >> 8p) & 255 (ascending digits = descending keys).  k_os_hist builds the
+// global histograms of every needed digit in one read.  Pass p: tiles of OS_TILE elements take
+// tickets in launch order; a tile ranks its elements stably ((round, wave) counts per digit + the
+// lane rank from a wave match), publishes its per-digit counts, looks back over its predecessors'
+// published counts for its exclusive offsets and scatters.  The look-back words are 8-byte granules
+// {epoch = pass + 1, flag, count} stored and polled with agent-scope atomics (sc1): the data is the
+// flag, so no fence is needed.  The granules are zeroed once per sort call (memset); a predecessor
+// always holds an earlier ticket, so it is resident and the wait ends.
+constexpr int OS_NT = 256;
+constexpr int OS_IPT = 16;
+constexpr int OS_TILE = OS_NT * OS_IPT;   // 4096
+constexpr int OS_NW = OS_NT / 64;
+constexpr uint64_t OS_AGG = 1ull << 32, OS_INC = 2ull << 32;
+constexpr uint32_t OS_SPIN_MAX = 1u << 26;
+// control words at the start of the look-back buffer (u64): [0, 2048) histograms (u32 pairs), tickets
+constexpr int OS_HIST_WORDS = 8 * 256 / 2;
+constexpr int OS_TICKET = OS_HIST_WORDS;          // 8 u32 tickets in 4 words
+constexpr int OS_ERR = OS_TICKET + 4;             // spin-limit flag
+constexpr int OS_HDR = OS_ERR + 4;                // 16-B aligned
 
-// per-tile histogram of digit (~key >> 8p) & 255, column-major [digit][tile]; pass p reads buffer p & 1
-__global__ __launch_bounds__(TK_NT) void k_sort_hist(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ k1,
-                                                      int64_t n, int p, const uint64_t* __restrict__ st,
-                                                      uint32_t* __restrict__ hist, int64_t ntiles) {
-    if (p >= sort_passes(st)) return;
-    const uint64_t* keys = (p & 1) ? k1 : k0;
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * TK_TILE;
-    const int shift = 8 * p;
-#pragma unroll
-    for (int j = 0; j < TK_IPT; j++) {
-        int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
-        if (i < n) atomicAdd(&h[((~keys[i]) >> shift) & 255], 1u);
-    }
-    __syncthreads();
-    hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+__device__ __forceinline__ void os_publish(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gu64_t*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t os_poll(const uint64_t* p) {
+    return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// stable scatter: tile elements processed in index order, rank among equal digits by
-// wave match (8 ballots) + per-wave LDS counts.
-__global__ __launch_bounds__(TK_NT) void k_sort_scatter(uint64_t* __restrict__ k0, uint32_t* __restrict__ v0,
-                                                         uint64_t* __restrict__ k1, uint32_t* __restrict__ v1,
-                                                         int64_t n, int p, const uint64_t* __restrict__ st,
-                                                         const uint32_t* __restrict__ hist, int64_t ntiles) {
+__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] + 7) / 8); }
+
+// histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
+// cluster); 16 loads in flight per thread
+__global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
+                                                   const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
+    __shared__ uint32_t h[8][256];
+    const int P = sort_passes(st);
+    for (int i = threadIdx.x; i < 8 * 256; i += OS_NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t lt = lanemask_lt();
+    const int64_t stride = (int64_t)gridDim.x * OS_NT;
+    for (int64_t i0 = (int64_t)blockIdx.x * OS_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
+        uint64_t kk[OS_IPT];
+#pragma unroll
+        for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~keys[i0 + r * stride] : 0ull;
+#pragma unroll
+        for (int r = 0; r < OS_IPT; r++) {
+            const bool valid = i0 + r * stride < n;
+            if (!__ballot(valid)) break;
+            for (int p = 0; p < P; p++) {
+                const int b = valid ? (int)((kk[r] >> (8 * p)) & 255) : -1;
+                const uint64_t act = __ballot(b >= 0);
+                const int b0 = __shfl(b, __builtin_ctzll(act), 64);
+                const uint64_t same = __ballot(b == b0);
+                if (b == b0) {
+                    if ((same & lt) == 0) atomicAdd(&h[p][b0], (uint32_t)__popcll(same));
+                } else if (b >= 0) {
+                    atomicAdd(&h[p][b], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t* gh = reinterpret_cast<uint32_t*>(lb);
+    for (int i = threadIdx.x; i < P * 256; i += OS_NT) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&gh[i], c);
+    }
+}
+
+__global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
+                                                   int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     if (p >= sort_passes(st)) return;
     const uint64_t* kin = (p & 1) ? k1 : k0;
     const uint32_t* vin = (p & 1) ? v1 : v0;
     uint64_t* kout = (p & 1) ? k0 : k1;
     uint32_t* vout = (p & 1) ? v0 : v1;
+    __shared__ uint16_t cnt[OS_IPT][OS_NW][256];   // (round, wave) counts per digit, then exclusive offsets
+    __shared__ uint32_t sbase[256];
+    __shared__ uint32_t lds[OS_NW + 1];
+    __shared__ uint32_t s_tile;
+    const int t = threadIdx.x, w = t >> 6;
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(lb + OS_TICKET);
+    if (t == 0) s_tile = atomicAdd(&ticket[p], 1u);
+    {
+        uint32_t* c32 = reinterpret_cast<uint32_t*>(&cnt[0][0][0]);
+        for (int i = t; i < OS_IPT * OS_NW * 128; i += OS_NT) c32[i] = 0;
+    }
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * OS_TILE;
     const int shift = 8 * p;
-    __shared__ uint32_t base_d[256];
-    __shared__ uint32_t wcnt[TK_NT / 64][256];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    base_d[t] = hist[(int64_t)t * ntiles + blockIdx.x];
-    const int64_t tile = (int64_t)blockIdx.x * TK_TILE;
-    for (int r = 0; r < TK_IPT; r++) {
-        for (int x = 0; x < TK_NT / 64; x++) wcnt[x][t] = 0;
-        __syncthreads();
-        int64_t i = tile + (int64_t)r * TK_NT + t;
-        bool valid = i < n;
-        uint64_t k = valid ? kin[i] : 0;
-        uint32_t v = valid ? vin[i] : 0;
-        uint32_t d = (uint32_t)(((~k) >> shift) & 255);
+    const uint64_t lt = lanemask_lt();
+    uint64_t kk[OS_IPT];
+    uint32_t vv[OS_IPT];
+    uint32_t rk[OS_IPT];   // digit | lane rank << 8
+#pragma unroll
+    for (int r = 0; r < OS_IPT; r++) {
+        const int64_t i = base + (int64_t)r * OS_NT + t;
+        kk[r] = i < n ? kin[i] : 0ull;
+        vv[r] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < OS_IPT; r++) {
+        const int64_t i = base + (int64_t)r * OS_NT + t;
+        const bool valid = i < n;
+        const uint32_t d = (uint32_t)(((~kk[r]) >> shift) & 255);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
-            uint64_t bb = __ballot((d >> b) & 1);
+            const uint64_t bb = __ballot((d >> b) & 1);
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
-        uint32_t rank = __popcll(peers & ((1ull << l) - 1));
-        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t off = base_d[d] + rank;
-            for (int x = 0; x < w; x++) off += wcnt[x][d];
-            kout[off] = k;
-            vout[off] = v;
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (valid && rank == 0) cnt[r][w][d] = (uint16_t)__popcll(peers);
+        rk[r] = d | (rank << 8);
+    }
+    __syncthreads();
+    // thread t owns digit t: exclusive offsets over (round, wave) in index order, tile aggregate
+    uint32_t agg = 0;
+#pragma unroll
+    for (int r = 0; r < OS_IPT; r++)
+#pragma unroll
+        for (int x = 0; x < OS_NW; x++) {
+            const uint32_t c = cnt[r][x][t];
+            cnt[r][x][t] = (uint16_t)agg;
+            agg += c;
         }
-        __syncthreads();
-        uint32_t add = 0;
-        for (int x = 0; x < TK_NT / 64; x++) add += wcnt[x][t];
-        base_d[t] += add;
+    const uint64_t ep = (uint64_t)(p + 1) << 34;
+    uint64_t* mine = lb + OS_HDR + tile * 256 + t;
+    uint32_t excl = 0;
+    if (tile == 0) {
+        os_publish(mine, ep | OS_INC | agg);
+    } else {
+        os_publish(mine, ep | OS_AGG | agg);
+        // look back over the predecessors, eight granules polled together: add counts until the first
+        // inclusive one; wait where a predecessor has not published yet
+        int64_t j = tile - 1;
+        uint32_t spins = 0;
+        for (;;) {
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = j - u >= 0 ? os_poll(lb + OS_HDR + (j - u) * 256 + t) : (ep | OS_INC);
+            int u = 0;
+            bool done = false;
+            for (; u < 8; u++) {
+                if ((v[u] >> 34) != (uint64_t)(p + 1)) break;
+                excl += (uint32_t)v[u];
+                if (v[u] & OS_INC) {
+                    done = true;
+                    break;
+                }
+            }
+            if (done) break;
+            j -= u;
+            if (u < 8 && ++spins > OS_SPIN_MAX) {   // bounded: a lost predecessor shows up as an error, not a hang
+                atomicOr(reinterpret_cast<uint32_t*>(lb + OS_ERR), 1u);
+                break;
+            }
+        }
+        os_publish(mine, ep | OS_INC | (uint64_t)(excl + agg));
+    }
+    // global start of each digit: exclusive scan of this pass's histogram
+    const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * 256;
+    uint32_t tot;
+    const uint32_t gstart = block_excl_scan<OS_NT>(gh[t], lds, &tot);
+    sbase[t] = gstart + excl;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < OS_IPT; r++) {
+        const int64_t i = base + (int64_t)r * OS_NT + t;
+        if (i < n) {
+            const uint32_t d = rk[r] & 255;
+            const uint32_t o = sbase[d] + cnt[r][w][d] + (rk[r] >> 8);
+            kout[o] = kk[r];
+            vout[o] = vv[r];
+        }
     }
 }
 
-__global__ void k_copy_idx(const uint32_t* v0, const uint32_t* v1, const uint64_t* st, uint32_t* out, int64_t n) {
+__global__ void k_copy_idx(const uint32_t* v0, const uint32_t* v1, const uint64_t* st, uint32_t* out, int64_t n,
+                           const uint64_t* lb, uint32_t* err) {
+    if (err && blockIdx.x == 0 && threadIdx.x == 0 && lb[OS_ERR]) atomicOr(err, 4u);
     const uint32_t* in = (sort_passes(st) & 1) ? v1 : v0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = in[i];
@@ -395,11 +511,10 @@ void TopkScratch::release() {
     v1.release();
     ck.release();
     ci.release();
-    tile_hist.release();
+    os.release();
     tile_a.release();
     tile_b.release();
     small.release();
-    scan.tiles.release();
 }
 
 __global__ void k_tk_range_reset(uint64_t* st) {
@@ -417,9 +532,8 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     s.ci.ensure(n);
     s.tile_a.ensure(n / TK_TILE + 1);
     s.tile_b.ensure(n / TK_TILE + 1);
-    s.tile_hist.ensure((size_t)(m / TK_TILE + 1) * 256);
+    s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * 256);
     s.small.ensure(ST_WORDS);
-    s.scan.tiles.ensure((size_t)((m / TK_TILE + 1) * 256) / 4096 + 1);
 }
 
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st) {
@@ -429,7 +543,7 @@ unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st) {
 }
 
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready) {
+                         hipStream_t st, bool range_ready, uint32_t* err) {
     if (n <= 0 || keep <= 0) return 0;
     const int64_t m = n < keep ? n : keep;
     s.k0.ensure(m);
@@ -479,16 +593,15 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m);
     }
     hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
-    const int64_t ntiles = (m + TK_TILE - 1) / TK_TILE;
-    s.tile_hist.ensure((size_t)ntiles * 256);
-    for (int p = 0; p < 8; p++) {
-        hipLaunchKernelGGL(k_sort_hist, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.k0.p, s.k1.p, m, p, stv,
-                           s.tile_hist.p, ntiles);
-        scan_exclusive_u32(s.tile_hist.p, s.tile_hist.p, ntiles * 256, nullptr, s.scan, st);
-        hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p,
-                           m, p, stv, s.tile_hist.p, ntiles);
-    }
-    hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m);
+    const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
+    const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
+    s.os.ensure(lb_words);
+    SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
+    hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, 256)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
+    for (int p = 0; p < 8; p++)
+        hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntiles), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+                           stv, s.os.p);
+    hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
     return m;
 }
