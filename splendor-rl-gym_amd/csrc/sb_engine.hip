@@ -12,8 +12,8 @@
 //                   survives iff it claimed and was never displaced: exactly
 //                   `if next_step in trail: continue` with first-occurrence order (src/solver.py:446-450)
 //   scan            survivor counts (cand & ~lost) -> next_queue offsets (parent rank, ordinal order)
-//   k_emit_q        survivors' packed states, parent links and heuristic scores, built densely from
-//                   an LDS queue; the noise of next_queue element k is the k-th accepted MT19937
+//   k_emit_w        survivors' packed states, parent links and heuristic scores, built densely 64 at a
+//                   time (sb_wave.inc); the noise of next_queue element k is the k-th accepted MT19937
 //                   draw (sb_mt.hip)
 //   top-k           stable descending sort + truncate (src/solver.py:452-456; sb_sort.hip)
 //   k_gather        the kept beam for the next turn + the per-pts first-rank table
@@ -202,9 +202,6 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
 #ifndef SB_XP_WAVES
 #define SB_XP_WAVES 1
 #endif
-#ifndef SB_EM_PAR
-#define SB_EM_PAR 32
-#endif
 #ifndef SB_XP_NT
 #define SB_XP_NT 256
 #endif
@@ -215,12 +212,6 @@ constexpr int XP_U = SB_XP_U;
 
 #ifndef SB_XP_GRID_CAP
 #define SB_XP_GRID_CAP (1u << 15)
-#endif
-#ifndef SB_WAVE_EXPAND
-#define SB_WAVE_EXPAND 0   // 1: wave-autonomous expansion (sb_wave.inc); 0: workgroup-queue form
-#endif
-#ifndef SB_WAVE_EMIT
-#define SB_WAVE_EMIT 1     // 1: wave-autonomous emission (sb_wave.inc); 0: workgroup-queue form
 #endif
 constexpr int XP_NT = SB_XP_NT;       // 4 waves
 constexpr int XP_PAR = SB_XP_PAR;     // parents per block iteration (<= 32)
@@ -283,14 +274,14 @@ __device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* 
 // Parents [0, n): every raw child is probed/claimed in the visited set; candidate bitmask (3 x u64)
 // per parent.  Successor order (src/solver.py:357-388) comes from masks: the buy set in deck order
 // (AND of per-colour affordability masks minus owned cards), then the valid take patterns of the
-// gem field in bucket order (Tables::tmask) — ordinal = rank in that order.
-// LM (lost marking): displaced same-turn claims are marked in `lost`; otherwise (sharded path) each
-// raw child's desc byte and visited slot are written at [rank*MAX_CHILDREN + ordinal].
-template <bool LM>
+// gem field in bucket order (Tables::tmask).  A child is named by its move descriptor dsc (card
+// 0..89, NCARDS + take-pattern bit): dsc order IS the canonical order, so the claim tag
+// (turn, parent rank, dsc) orders exactly like (turn, parent rank, ordinal), and the candidate /
+// lost bits of a parent are indexed by dsc (the 192-bit move space of move_space()).
+// Displaced same-turn claims are marked in `lost` (lost marking).
 __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
-                                                  uint64_t mask, uint64_t turn_tag, uint8_t* __restrict__ desc,
-                                                  uint32_t* __restrict__ rslot, unsigned long long* __restrict__ cand,
+                                                  uint64_t mask, uint64_t turn_tag, unsigned long long* __restrict__ cand,
                                                   unsigned long long* __restrict__ lost,
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err) {
     __shared__ XpShared S;
@@ -356,22 +347,18 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                 atomicAdd(&S.nraw, (uint32_t)tot);
             }
             qb = __shfl(qb, 0, 64);
-            uint8_t* dr = LM ? nullptr : desc + r * MAX_CHILDREN;
-            auto put = [&](int o, int dsc) {
-                S.q[qb + o] = (uint32_t)s | ((uint32_t)o << 5) | ((uint32_t)dsc << 13);
-                if constexpr (!LM) dr[o] = (uint8_t)dsc;
-            };
+            auto put = [&](int o, int dsc) { S.q[qb + o] = (uint32_t)s | ((uint32_t)dsc << 5); };
             if ((bl >> lane) & 1) put(__popcll(bl & lt), lane);
             if (lane < 26 && ((bh >> lane) & 1)) put(nbl + __popc(bh & (uint32_t)lt), 64 + lane);
             if ((t0 >> lane) & 1) put(nb + __popcll(t0 & lt), NCARDS + lane);
             if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
         }
         __syncthreads();
-        // ---- phase B: dense child processing: key, visited probe + claim.  LM: XP_U children per
-        // thread with their first probe loads issued together (more misses in flight per wave).
+        // ---- phase B: dense child processing: key, visited probe + claim; XP_U children per thread
+        // with their first probe loads issued together (more misses in flight per wave).
         const uint32_t nq = S.nq;
         auto child_key = [&](uint32_t e) -> uint64_t {
-            const int s = (int)(e & 31), dsc = (int)(e >> 13);
+            const int s = (int)(e & 31), dsc = (int)(e >> 5);
             const uint64_t lo = S.plo[s], hi = S.phi[s];
             if (dsc < NCARDS) {
                 Derived d;
@@ -383,40 +370,26 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             const uint32_t gf = (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]);
             return state_key(S.phc[s], hash_gems(gf));
         };
-        if constexpr (LM) {
-            for (uint32_t i0 = t; i0 < nq; i0 += XP_NT * XP_U) {
-                uint32_t e[XP_U];
-                uint64_t key[XP_U];
-                ulonglong2 ent[XP_U];
+        for (uint32_t i0 = t; i0 < nq; i0 += XP_NT * XP_U) {
+            uint32_t e[XP_U];
+            uint64_t key[XP_U];
+            ulonglong2 ent[XP_U];
 #pragma unroll
-                for (int u = 0; u < XP_U; u++) {
-                    const uint32_t i = i0 + u * XP_NT;
-                    e[u] = i < nq ? S.q[i] : 0xFFFFFFFFu;
-                    key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < XP_U; u++)
-                    if (e[u] != 0xFFFFFFFFu) ent[u] = *reinterpret_cast<const ulonglong2*>(&tab[mix64(key[u]) & mask]);
-#pragma unroll
-                for (int u = 0; u < XP_U; u++) {
-                    if (e[u] == 0xFFFFFFFFu) continue;
-                    const int s = (int)(e[u] & 31), o = (int)((e[u] >> 5) & 255);
-                    const uint64_t tag = turn_tag | ((uint64_t)(base + s) << 8) | (uint64_t)o;
-                    if (visit_claim_lm_pre(tab, mask, key[u], ent[u], tag, lost, err))
-                        atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
-                }
+            for (int u = 0; u < XP_U; u++) {
+                const uint32_t i = i0 + u * XP_NT;
+                e[u] = i < nq ? S.q[i] : 0xFFFFFFFFu;
+                key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
             }
-        } else {
-            for (uint32_t i = t; i < nq; i += XP_NT) {
-                const uint32_t e = S.q[i];
-                const int s = (int)(e & 31), o = (int)((e >> 5) & 255);
-                const uint64_t key = child_key(e);
-                const int64_t r = base + s;
-                const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
-                uint32_t slot;
-                const bool c = visit_claim(tab, mask, key, tag, &slot, err);
-                rslot[r * MAX_CHILDREN + o] = slot;
-                if (c) atomicOr(&S.cmask[s][o >> 6], 1ull << (o & 63));
+#pragma unroll
+            for (int u = 0; u < XP_U; u++)
+                if (e[u] != 0xFFFFFFFFu) ent[u] = *reinterpret_cast<const ulonglong2*>(&tab[mix64(key[u]) & mask]);
+#pragma unroll
+            for (int u = 0; u < XP_U; u++) {
+                if (e[u] == 0xFFFFFFFFu) continue;
+                const int s = (int)(e[u] & 31), dsc = (int)(e[u] >> 5);
+                const uint64_t tag = turn_tag | ((uint64_t)(base + s) << 8) | (uint64_t)dsc;
+                if (visit_claim_lm_pre(tab, mask, key[u], ent[u], tag, lost, err))
+                    atomicOr(&S.cmask[s][dsc >> 6], 1ull << (dsc & 63));
             }
         }
         __syncthreads();
@@ -463,188 +436,6 @@ __global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
         cnt[r] = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
                  __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
-}
-
-// rank of ordinal o among the set bits of the 192-bit mask (m0, m1, m2)
-__device__ __forceinline__ uint32_t mask_rank(uint64_t m0, uint64_t m1, uint64_t m2, int o) {
-    const uint64_t below = (1ull << (o & 63)) - 1;
-    if (o < 64) return __popcll(m0 & below);
-    if (o < 128) return __popcll(m0) + __popcll(m1 & below);
-    return __popcll(m0) + __popcll(m1) + __popcll(m2 & below);
-}
-__device__ __forceinline__ bool mask_bit(uint64_t m0, uint64_t m1, uint64_t m2, int o) {
-    const uint64_t m = o < 64 ? m0 : (o < 128 ? m1 : m2);
-    return (m >> (o & 63)) & 1;
-}
-
-// ------------------------------------------------------------------ k_emit_q (block queue, dense children)
-// Phase A: a wave per parent re-enumerates its children in canonical order and queues the survivors
-// (cand & ~lost) with their rank inside the parent.  Phase B: all threads build the queued children
-// densely — state, parent link, float64 score with the MT noise of its next_queue position.
-constexpr int EM_PAR = SB_EM_PAR;   // <= 32
-struct EmShared {
-    uint32_t card[NCARDS];
-    int32_t pdelta[4][NPAT_MAX];
-    uint64_t mlo[NCOL];
-    uint32_t mhi[NCOL];
-    uint64_t alo[NCOL][8];
-    uint32_t ahi[NCOL][8];
-    uint64_t sm[EM_PAR][3];
-    uint64_t plo[EM_PAR], phi[EM_PAR];
-    uint64_t ptm[EM_PAR][2];
-    uint64_t pbl[EM_PAR];
-    uint32_t pbh[EM_PAR];
-    uint32_t poff[EM_PAR];
-    uint32_t pbon[EM_PAR];
-    int32_t pbk[EM_PAR];
-    uint32_t q[EM_PAR * MAX_CHILDREN];
-    uint32_t nq;
-};
-
-template <int H>
-__global__ __launch_bounds__(256) void k_emit_q(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
-                                                const uint64_t* __restrict__ bhi, int64_t n,
-                                                const unsigned long long* __restrict__ cand,
-                                                const unsigned long long* __restrict__ lost,
-                                                const uint32_t* __restrict__ off, uint64_t* __restrict__ nlo,
-                                                uint64_t* __restrict__ nhi, uint32_t* __restrict__ npar,
-                                                uint64_t* __restrict__ skey, const uint8_t* __restrict__ ring,
-                                                uint64_t ring_mask, uint64_t ring_base, uint32_t par_base,
-                                                uint32_t* __restrict__ err, unsigned long long* __restrict__ krange) {
-    __shared__ EmShared S;
-    __shared__ unsigned long long kmin, kmax;   // key range for the top-k (sb_sort.hip), one atomic pair per block
-    if (threadIdx.x == 0) {
-        kmin = ~0ull;
-        kmax = 0;
-    }
-    uint64_t tmin = ~0ull, tmax = 0;
-    load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint64_t lt = lanemask_lt();
-    // per-parent inputs of a group, one value per thread: t < 96 survivor masks, then lo, hi, off
-    auto fetch = [&](int64_t b) -> uint64_t {
-        if (t < 3 * EM_PAR) {
-            const int64_t i = b * 3 + t;
-            return i < n * 3 ? (uint64_t)(cand[i] & ~lost[i]) : 0ull;
-        }
-        const int j = t - 3 * EM_PAR, s = j & (EM_PAR - 1);
-        const int64_t r = b + s;
-        if (r >= n || j >= 3 * EM_PAR) return 0ull;
-        return j < EM_PAR ? blo[r] : (j < 2 * EM_PAR ? bhi[r] : (uint64_t)off[r]);
-    };
-    int64_t base = (int64_t)blockIdx.x * EM_PAR;
-    uint64_t pf = base < n ? fetch(base) : 0ull;
-    for (; base < n; base += (int64_t)gridDim.x * EM_PAR) {
-        if (t == 0) S.nq = 0;
-        if (t < 3 * EM_PAR) (&S.sm[0][0])[t] = pf;
-        else if (t < 6 * EM_PAR) {
-            const int j = t - 3 * EM_PAR, s = j & (EM_PAR - 1);
-            if (j < EM_PAR) S.plo[s] = pf;
-            else if (j < 2 * EM_PAR) S.phi[s] = pf;
-            else S.poff[s] = (uint32_t)pf;
-        }
-        __syncthreads();
-        const int64_t nb_ = base + (int64_t)gridDim.x * EM_PAR;
-        if (nb_ < n) pf = fetch(nb_);   // next group's inputs load under this group's work
-        // prologue, a lane per parent with survivors: buy set, bucket, take mask, packed bonus
-        if (t < EM_PAR && (S.sm[t][0] | S.sm[t][1] | S.sm[t][2])) {
-            const uint64_t lo = S.plo[t], hi = S.phi[t];
-            Derived d;
-            derive_lds(S.mlo, S.mhi, lo, hi, d);
-            uint64_t bl;
-            uint32_t bh;
-            buy_set(S.alo, S.ahi, d, lo, hi, &bl, &bh);
-            const int bk = take_bucket(d);
-            uint64_t t0 = 0, t1 = 0;
-            if (bk >= 0) {
-                const uint32_t gf = st_gemfield(hi);
-                t0 = T->tmask[gf][0];
-                t1 = T->tmask[gf][1];
-            }
-            S.pbl[t] = bl;
-            S.pbh[t] = bh;
-            S.ptm[t][0] = t0;
-            S.ptm[t][1] = t1;
-            S.pbon[t] = pack_bonus(d);
-            S.pbk[t] = bk;
-        }
-        __syncthreads();
-        // ---- phase A: a wave per parent queues its surviving children with their rank
-        for (int s = w; s < EM_PAR; s += 4) {
-            const int64_t r = base + s;
-            if (r >= n) break;
-            const uint64_t m0 = S.sm[s][0], m1 = S.sm[s][1], m2 = S.sm[s][2];
-            if ((m0 | m1 | m2) == 0) continue;
-            const uint64_t bl = S.pbl[s], t0 = S.ptm[s][0], t1 = S.ptm[s][1];
-            const uint32_t bh = S.pbh[s];
-            const int nbl = __popcll(bl), nb = nbl + __popc(bh), nt0 = __popcll(t0);
-            uint32_t qb = 0;
-            if (lane == 0) qb = atomicAdd(&S.nq, (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2)));
-            qb = __shfl(qb, 0, 64);
-            auto put = [&](int o, int dsc) {
-                if (mask_bit(m0, m1, m2, o)) {
-                    const uint32_t rk = mask_rank(m0, m1, m2, o);
-                    S.q[qb + rk] = (uint32_t)s | ((uint32_t)dsc << 5) | (rk << 13);
-                }
-            };
-            if ((bl >> lane) & 1) put(__popcll(bl & lt), lane);
-            if (lane < 26 && ((bh >> lane) & 1)) put(nbl + __popc(bh & (uint32_t)lt), 64 + lane);
-            if ((t0 >> lane) & 1) put(nb + __popcll(t0 & lt), NCARDS + lane);
-            if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
-        }
-        __syncthreads();
-        // ---- phase B: build the queued children densely
-        const uint32_t nq = S.nq;
-        for (uint32_t i = t; i < nq; i += 256) {
-            const uint32_t e = S.q[i];
-            const int s = (int)(e & 31), dsc = (int)((e >> 5) & 255);
-            const uint32_t kk = S.poff[s] + (e >> 13);
-            int nv = 1;
-            if constexpr (H >= 0) nv = ring[(ring_base + kk) & ring_mask];
-            const uint64_t lo = S.plo[s], hi = S.phi[s];
-            Derived d;
-            derive_packed(hi, S.pbon[s], d);
-            int B = 0, U = 0;
-#pragma unroll
-            for (int c = 0; c < NCOL; c++) {
-                B += d.b[c];
-                U += d.b[c] > 0;
-            }
-            uint64_t clo = lo, chi;
-            if (dsc < NCARDS) {
-                const uint32_t cw = S.card[dsc];
-                chi = buy_child_hi(cw, dsc, d, hi, &clo);
-                B += 1;
-                U += ((S.pbon[s] >> (5 * card_color(cw))) & 31) == 0;   // (no dynamic index into d.b)
-            } else {
-                chi = st_with_gems(hi, (uint32_t)((int32_t)st_gemfield(hi) + S.pdelta[S.pbk[s]][dsc - NCARDS]));
-            }
-            nlo[kk] = clo;
-            nhi[kk] = chi;
-            npar[kk] = par_base + (uint32_t)(base + s);
-            if constexpr (H >= 0) {
-                if (st_saved(chi) >= POW_BASES) atomicOr(err, 2u);
-                int G = 0;
-#pragma unroll
-                for (int c = 0; c < NCOL; c++) G += st_gem(chi, c);
-                const double sc = score_vals<H>(T->pw, st_pts(chi), st_saved(chi), G, B, U, T->noise[nv - 1]);
-                const uint64_t key = (uint64_t)__double_as_longlong(sc);
-                skey[kk] = key;
-                tmin = key < tmin ? key : tmin;
-                tmax = key > tmax ? key : tmax;
-            }
-        }
-        __syncthreads();
-    }
-    if constexpr (H >= 0) {
-        atomicMin(&kmin, (unsigned long long)tmin);
-        atomicMax(&kmax, (unsigned long long)tmax);
-        __syncthreads();
-        if (threadIdx.x == 0 && kmax >= kmin) {
-            atomicMin(&krange[0], kmin);
-            atomicMax(&krange[1], kmax);
-        }
-    }
 }
 
 #include "sb_wave.inc"
@@ -900,6 +691,7 @@ static void check_err_word(Engine& E) {
     if (e & 1u) throw HipError{hipErrorOutOfMemory, "visited set overfull (probe limit); raise visited_log2"};
     if (e & 2u) throw HipError{hipErrorInvalidValue, "saved >= 256 exceeds the pow tables"};
     if (e & 4u) throw HipError{hipErrorLaunchFailure, "top-k sort look-back wait exceeded its bound"};
+    if (e & 8u) throw HipError{hipErrorLaunchFailure, "sharded answers do not match the parents' move counts"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -959,15 +751,10 @@ static void launch_front(Engine& E) {
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
     if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
     if (n > 0) {
-        if (SB_WAVE_EXPAND)
-            hipLaunchKernelGGL(k_expand_w, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi,
-                               n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
-        else
-            // grid-stride over groups of XP_PAR parents (an uncapped one-group-per-block grid measured
-            // slower: same-turn duplicates come from all over the beam, not from nearby ranks)
-            hipLaunchKernelGGL(k_expand<true>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
-                               cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, (uint8_t*)nullptr, (uint32_t*)nullptr,
-                               E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
+        // grid-stride over groups of XP_PAR parents (an uncapped one-group-per-block grid measured
+        // slower: same-turn duplicates come from all over the beam, not from nearby ranks)
+        hipLaunchKernelGGL(k_expand, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
+                           cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)
@@ -1063,9 +850,9 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
     if (timing) SB_HIP(hipEventRecord(ev[3], E.s));
     const double h2 = hnow();
-    const unsigned eg = SB_WAVE_EMIT ? grid_cap(n, 256, 8192) : grid_cap(n, EM_PAR, 1u << 15);
+    const unsigned eg = grid_cap(n, 256, 8192);
     const uint64_t rbase = E.noise.consumed;
-#define EMIT_K(H) (SB_WAVE_EMIT ? k_emit_w<H> : k_emit_q<H>)
+#define EMIT_K(H) k_emit_w<H>
     if (!heur) {
         hipLaunchKernelGGL(EMIT_K(-1), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, E.lost.p,
                            E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase, 0u,
