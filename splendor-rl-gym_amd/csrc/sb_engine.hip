@@ -51,33 +51,6 @@ struct alignas(16) Entry {
 constexpr int MAX_PROBE = 4096;
 
 // ------------------------------------------------------------------ visited-set probe
-// Returns true if the child is a candidate first occurrence (its tag may win the claim).
-__device__ __forceinline__ bool visit_claim(Entry* __restrict__ tab, uint64_t mask, uint64_t key, uint64_t tag,
-                                            uint32_t* slot_out, uint32_t* err) {
-    uint64_t h = mix64(key) & mask;
-    for (int probe = 0;; probe++) {
-        uint64_t k = tab[h].key;   // a stale EMPTY is resolved by the CAS; keys never change once set
-        if (k == EMPTY) {
-            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
-                                      (unsigned long long)key);
-            if (prev == EMPTY || prev == key) break;
-            k = prev;
-        }
-        if (k == key) break;
-        h = (h + 1) & mask;
-        if (probe >= MAX_PROBE) {
-            atomicOr(err, 1u);
-            *slot_out = 0xFFFFFFFFu;
-            return false;
-        }
-    }
-    *slot_out = (uint32_t)h;
-    uint64_t cur = tab[h].tag;   // stale reads only over-estimate (EMPTY or a larger same-turn tag)
-    if (cur != EMPTY && cur < tag) return false;   // seen in an earlier turn, or claimed earlier this turn
-    atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
-    return true;
-}
-
 // Claim with displacement marking (single-GPU speedrun path).  The winner of a key within a turn is
 // the smallest tag (parent rank, ordinal) — the reference's first occurrence in next_queue order.  A
 // claimant that lowers a same-turn tag marks the displaced holder in `lost`; one whose atomicMin finds
@@ -400,34 +373,6 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
         __syncthreads();
     }
     if (t == 0 && S.nraw) atomicAdd(nraw_total, (unsigned long long)S.nraw);
-}
-
-// ------------------------------------------------------------------ k_survive (wave per parent)
-__global__ __launch_bounds__(256) void k_survive(int64_t n, const Entry* __restrict__ tab, uint64_t turn_tag,
-                                                  const uint32_t* __restrict__ rslot,
-                                                  const unsigned long long* __restrict__ cand,
-                                                  unsigned long long* __restrict__ surv, uint32_t* __restrict__ cnt) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t r = wg; r < n; r += nw) {
-        uint32_t total = 0;
-#pragma unroll
-        for (int pass = 0; pass < 3; pass++) {
-            const unsigned long long cm = cand[r * 3 + pass];
-            bool sv = false;
-            if ((cm >> lane) & 1ull) {
-                const int o = pass * 64 + lane;
-                const uint32_t slot = rslot[r * MAX_CHILDREN + o];
-                const uint64_t tag = turn_tag | ((uint64_t)r << 8) | (uint64_t)o;
-                sv = tab[slot].tag == tag;
-            }
-            const unsigned long long m = __ballot(sv);
-            if (lane == 0) surv[r * 3 + pass] = m;
-            total += __popcll(m);
-        }
-        if (lane == 0) cnt[r] = total;
-    }
 }
 
 // ------------------------------------------------------------------ survivors of the lost-marking path
