@@ -17,6 +17,11 @@ import torch.distributed as dist
 
 
 def main(args):
+    import sys
+    # RCCL prints its version banner on stdout at init: keep stdout for the one JSON line
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     from bench import HBM_PEAK_GBS, METRIC, step_bytes
     from splendor_amd.dist import Comm, DistSolve, HipBackend
     from splendor_amd.engine import HEURISTIC_IDS
@@ -58,7 +63,6 @@ def main(args):
     uniq = sum(p['n_unique'] for p in per)
     kept = sum(p['n_kept'] for p in per)
     if rank == 0 and os.environ.get('SB_DIST_PHASES') == '1':
-        import sys
         for p in per:
             print('phases', p.get('phases'), file=sys.stderr, flush=True)
     if rank == 0:
@@ -79,6 +83,8 @@ def main(args):
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
             'cpu_baseline': None,
         }
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)
     b.close()
     dist.destroy_process_group()

@@ -203,8 +203,9 @@ struct XpShared {
     uint32_t pbon[XP_PAR];
     int32_t pbk[XP_PAR];
     unsigned long long cmask[XP_PAR][3];
-    uint32_t q[XP_PAR * MAX_CHILDREN];
-    uint32_t nq, nraw;
+    uint32_t qb[XP_PAR * NCARDS];     // buy children (s | dsc << 5)
+    uint32_t qt[XP_PAR * NPAT_MAX];   // take children: phase B runs all buys, then all takes, so a
+    uint32_t nqb, nqt, nraw;          // wave rarely mixes the two (a buy re-hashes its card tuple)
 };
 
 // enumeration tables into LDS: cards, colour masks, affordability masks, pattern deltas
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
     int64_t base = (int64_t)blockIdx.x * XP_PAR;
     uint64_t pf = base < n ? fetch(base) : 0ull;
     for (; base < n; base += (int64_t)gridDim.x * XP_PAR) {
-        if (t == 0) S.nq = 0;
+        if (t == 0) S.nqb = S.nqt = 0;
         if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
         if (t < XP_PAR) S.plo[t] = pf;
         else if (t < 2 * XP_PAR) S.phi[t - XP_PAR] = pf;
@@ -313,23 +314,25 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             const uint64_t bl = S.pbl[s], t0 = S.ptm[s][0], t1 = S.ptm[s][1];
             const uint32_t bh = S.pbh[s];
             const int nbl = __popcll(bl), nb = nbl + __popc(bh), nt0 = __popcll(t0);
-            const int tot = nb + nt0 + __popcll(t1);
-            uint32_t qb = 0;
+            const int nt = nt0 + __popcll(t1);
+            uint32_t qb = 0, qt = 0;
             if (lane == 0) {
-                qb = atomicAdd(&S.nq, (uint32_t)tot);
-                atomicAdd(&S.nraw, (uint32_t)tot);
+                qb = atomicAdd(&S.nqb, (uint32_t)nb);
+                qt = atomicAdd(&S.nqt, (uint32_t)nt);
+                atomicAdd(&S.nraw, (uint32_t)(nb + nt));
             }
             qb = __shfl(qb, 0, 64);
-            auto put = [&](int o, int dsc) { S.q[qb + o] = (uint32_t)s | ((uint32_t)dsc << 5); };
-            if ((bl >> lane) & 1) put(__popcll(bl & lt), lane);
-            if (lane < 26 && ((bh >> lane) & 1)) put(nbl + __popc(bh & (uint32_t)lt), 64 + lane);
-            if ((t0 >> lane) & 1) put(nb + __popcll(t0 & lt), NCARDS + lane);
-            if ((t1 >> lane) & 1) put(nb + nt0 + __popcll(t1 & lt), NCARDS + 64 + lane);
+            qt = __shfl(qt, 0, 64);
+            if ((bl >> lane) & 1) S.qb[qb + __popcll(bl & lt)] = (uint32_t)s | ((uint32_t)lane << 5);
+            if (lane < 26 && ((bh >> lane) & 1))
+                S.qb[qb + nbl + __popc(bh & (uint32_t)lt)] = (uint32_t)s | ((uint32_t)(64 + lane) << 5);
+            if ((t0 >> lane) & 1) S.qt[qt + __popcll(t0 & lt)] = (uint32_t)s | ((uint32_t)(NCARDS + lane) << 5);
+            if ((t1 >> lane) & 1) S.qt[qt + nt0 + __popcll(t1 & lt)] = (uint32_t)s | ((uint32_t)(NCARDS + 64 + lane) << 5);
         }
         __syncthreads();
         // ---- phase B: dense child processing: key, visited probe + claim; XP_U children per thread
         // with their first probe loads issued together (more misses in flight per wave).
-        const uint32_t nq = S.nq;
+        const uint32_t nqb = S.nqb, nq = nqb + S.nqt;
         auto child_key = [&](uint32_t e) -> uint64_t {
             const int s = (int)(e & 31), dsc = (int)(e >> 5);
             const uint64_t lo = S.plo[s], hi = S.phi[s];
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
 #pragma unroll
             for (int u = 0; u < XP_U; u++) {
                 const uint32_t i = i0 + u * XP_NT;
-                e[u] = i < nq ? S.q[i] : 0xFFFFFFFFu;
+                e[u] = i < nqb ? S.qb[i] : (i < nq ? S.qt[i - nqb] : 0xFFFFFFFFu);
                 key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
             }
 #pragma unroll
