@@ -409,6 +409,44 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t* __restrict__ idx
     if (f[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&first[threadIdx.x], f[threadIdx.x]);
 }
 
+// kept beam rebuilt from descriptors (parent rank << 8 | dsc) + the per-pts first-rank table
+__global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, const uint32_t* __restrict__ idx, int64_t m,
+                                                  const uint64_t* __restrict__ ndesc, const uint64_t* __restrict__ plo,
+                                                  const uint64_t* __restrict__ phi, uint64_t* __restrict__ olo,
+                                                  uint64_t* __restrict__ ohi, uint32_t* __restrict__ opar,
+                                                  uint32_t* __restrict__ first) {
+    __shared__ uint32_t f[256];
+    __shared__ uint32_t card[NCARDS];
+    __shared__ int32_t pdelta[4][NPAT_MAX];
+    __shared__ uint64_t mlo[NCOL];
+    __shared__ uint32_t mhi[NCOL];
+    f[threadIdx.x] = 0xFFFFFFFFu;
+    for (int i = threadIdx.x; i < NCARDS; i += blockDim.x) card[i] = T->card[i];
+    for (int i = threadIdx.x; i < 4 * NPAT_MAX; i += blockDim.x) (&pdelta[0][0])[i] = (&T->pdelta[0][0])[i];
+    if (threadIdx.x < NCOL) {
+        mlo[threadIdx.x] = T->colmask_lo[threadIdx.x];
+        mhi[threadIdx.x] = T->colmask_hi[threadIdx.x];
+    }
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t dd = ndesc[idx[i]];
+        const uint32_t r = (uint32_t)(dd >> 8);
+        const int dsc = (int)(dd & 255);
+        const uint64_t lo = plo[r], hi = phi[r];
+        Derived d;
+        derive_lds(mlo, mhi, lo, hi, d);
+        uint64_t clo = lo, chi;
+        if (dsc < NCARDS) chi = buy_child_hi(card[dsc], dsc, d, hi, &clo);
+        else chi = st_with_gems(hi, (uint32_t)((int32_t)st_gemfield(hi) + pdelta[take_bucket(d)][dsc - NCARDS]));
+        olo[i] = clo;
+        ohi[i] = chi;
+        opar[i] = r;
+        atomicMin(&f[st_pts(chi)], (uint32_t)i);
+    }
+    __syncthreads();
+    if (f[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&first[threadIdx.x], f[threadIdx.x]);
+}
+
 __global__ void k_pts_first(const uint64_t* __restrict__ bhi, int64_t m, uint32_t* __restrict__ first) {
     __shared__ uint32_t f[256];
     f[threadIdx.x] = 0xFFFFFFFFu;
@@ -809,7 +847,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         unsigned long long* krange = topk_range_reset(E.topk, E.s);
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
-    hipLaunchKernelGGL(EMIT_K(H), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p,          \
+    hipLaunchKernelGGL((k_emit_w<H, false>), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, \
                        E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
                        rbase, 0u, E.d_small + 1, krange);                                                         \
     break;
@@ -838,8 +876,12 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     nt.par = (uint32_t*)E.turn_mem.alloc(m * 4);
     nt.n = m;
     SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
-    hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
-                       nt.lo, nt.hi, nt.par, E.d_small + 8);
+    if (heur)   // emission wrote descriptors only: rebuild the kept states from their parents
+        hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
+                           cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8);
+    else
+        hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
+                           nt.lo, nt.hi, nt.par, E.d_small + 8);
     if (timing) SB_HIP(hipEventRecord(ev[6], E.s));
     SB_HIP(hipGetLastError());
     E.turns.push_back(nt);
