@@ -184,7 +184,7 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
 constexpr int XP_U = SB_XP_U;
 
 #ifndef SB_XP_GRID_CAP
-#define SB_XP_GRID_CAP (1u << 15)
+#define SB_XP_GRID_CAP 2560   // ~2 blocks per resident slot (5 per CU); groups come from a counter
 #endif
 constexpr int XP_NT = SB_XP_NT;       // 4 waves
 constexpr int XP_PAR = SB_XP_PAR;     // parents per block iteration (<= 32)
@@ -206,6 +206,7 @@ struct XpShared {
     uint32_t qb[XP_PAR * NCARDS];     // buy children (s | dsc << 5)
     uint32_t qt[XP_PAR * NPAT_MAX];   // take children: phase B runs all buys, then all takes, so a
     uint32_t nqb, nqt, nraw;          // wave rarely mixes the two (a buy re-hashes its card tuple)
+    uint32_t grp[3];                  // this, next and next-but-one parent group
 };
 
 // enumeration tables into LDS: cards, colour masks, affordability masks, pattern deltas
@@ -257,7 +258,8 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
                                                   uint64_t mask, uint64_t turn_tag, unsigned long long* __restrict__ cand,
                                                   unsigned long long* __restrict__ lost,
-                                                  unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err) {
+                                                  unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err,
+                                                  uint32_t* __restrict__ work) {
     __shared__ XpShared S;
     load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -269,18 +271,26 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
         if (t >= 2 * XP_PAR || r >= n) return 0ull;
         return t < XP_PAR ? blo[r] : bhi[r];
     };
-    int64_t base = (int64_t)blockIdx.x * XP_PAR;
+    // groups are handed out in rank order by a counter (not a grid stride), so claims run roughly in
+    // tag order and fewer same-turn holders get displaced; each block fetches a group ahead
+    if (t == 0) {
+        S.grp[0] = atomicAdd(work, 1u);
+        S.grp[1] = atomicAdd(work, 1u);
+    }
+    __syncthreads();
+    int64_t base = (int64_t)S.grp[0] * XP_PAR, nxt = (int64_t)S.grp[1] * XP_PAR;
     uint64_t pf = base < n ? fetch(base) : 0ull;
-    for (; base < n; base += (int64_t)gridDim.x * XP_PAR) {
-        if (t == 0) S.nqb = S.nqt = 0;
+    while (base < n) {
+        if (t == 0) {
+            S.nqb = S.nqt = 0;
+            S.grp[2] = atomicAdd(work, 1u);   // the group after next; read after the barrier below
+        }
         if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
         if (t < XP_PAR) S.plo[t] = pf;
         else if (t < 2 * XP_PAR) S.phi[t - XP_PAR] = pf;
         __syncthreads();
-        {
-            const int64_t nb = base + (int64_t)gridDim.x * XP_PAR;
-            if (nb < n) pf = fetch(nb);
-        }
+        const int64_t nxt2 = (int64_t)S.grp[2] * XP_PAR;
+        if (nxt < n) pf = fetch(nxt);
         // prologue, a lane per parent: buy set, bucket, take mask, packed bonus, hash of the card tuple
         if (t < XP_PAR) {
             const uint64_t lo = S.plo[t], hi = S.phi[t];
@@ -374,6 +384,8 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             if (base + s < n) cand[(base + s) * 3 + j] = S.cmask[s][j];
         }
         __syncthreads();
+        base = nxt;
+        nxt = nxt2;
     }
     if (t == 0 && S.nraw) atomicAdd(nraw_total, (unsigned long long)S.nraw);
 }
@@ -632,7 +644,7 @@ struct Engine {
     DBuf<uint32_t> cnt, off;
     DBuf<uint64_t> nlo, nhi, skey;
     DBuf<uint32_t> npar, kidx;
-    uint32_t* d_small = nullptr;            // [0] n_unique total  [1] err  [2..] pad ; [8..8+256) first-rank table
+    uint32_t* d_small = nullptr;            // [0] n_unique total  [1] err  [2..8) claim stats ; [8..8+256) first-rank table ; [264] k_expand group counter
     unsigned long long* d_nraw = nullptr;
     uint32_t* h_small = nullptr;            // pinned mirror of d_small (264 words)
     unsigned long long* h_nraw = nullptr;
@@ -734,13 +746,15 @@ static void launch_front(Engine& E) {
     SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
     SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
     SB_HIP(hipMemsetAsync(E.d_small + 2, 0, 6 * 4, E.s));   // claim statistics (SB_CLAIM_STATS builds): [2..8)
+    SB_HIP(hipMemsetAsync(E.d_small + 264, 0, 4, E.s));     // k_expand's group counter
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
     if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
     if (n > 0) {
-        // grid-stride over groups of XP_PAR parents (an uncapped one-group-per-block grid measured
-        // slower: same-turn duplicates come from all over the beam, not from nearby ranks)
+        // a capped grid pulling groups of XP_PAR parents from a counter in rank order (a grid-stride
+        // walk ran blocks a million ranks apart side by side: more displaced same-turn claims)
         hipLaunchKernelGGL(k_expand, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
-                           cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1);
+                           cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1,
+                           E.d_small + 264);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)
@@ -808,6 +822,10 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         }
     }
     check_err_word(E);
+#ifdef SB_CLAIM_STATS
+    fprintf(stderr, "claims turn %d: old %u inserted %u early-out %u lost-at-min %u displaced %u\n", E.turn,
+            E.h_small[3], E.h_small[4], E.h_small[5], E.h_small[6], E.h_small[7]);
+#endif
     const bool heur = E.cfg.use_heuristic != 0;
     const int64_t nu = E.h_small[0];
     out->n_raw = (int64_t)*E.h_nraw;
@@ -1036,7 +1054,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
             SB_HIP(hipMalloc((void**)&E.own, cap * sizeof(Entry)));
             SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
         }
-        SB_HIP(hipMalloc((void**)&E.d_small, 264 * 4));
+        SB_HIP(hipMalloc((void**)&E.d_small, 272 * 4));
         SB_HIP(hipMalloc((void**)&E.d_nraw, 8));
         SB_HIP(hipHostMalloc((void**)&E.h_small, 264 * 4, hipHostMallocDefault));
         SB_HIP(hipHostMalloc((void**)&E.h_nraw, 8, hipHostMallocDefault));
