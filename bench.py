@@ -37,7 +37,7 @@ def parse():
     ap.add_argument('--heuristic', default='balanced')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-budget-s', type=float, default=20.0)
+    ap.add_argument('--cpu-budget-s', type=float, default=30.0)
     ap.add_argument('--realistic', action='store_true',
                     help='config C4 instead: realistic 2-player goal 15 --shuffle, W=1M (a separate line, not the '
                          'headline metric)')
