@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(REPO, 'oracle'))
 
 METRIC = 'states expanded/sec per beam step, goal=15 beam_width=4M, 1/2/4/8 MI355X'
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+RANDOM_LOAD_PEAK_G = 48.0   # random 16-B loads / s over a 32 GiB table, measured (profiles/micro/r1_randaccess.txt)
 
 
 def parse():
@@ -222,6 +223,15 @@ def main():
         'step_model_GBps': round(step_bytes(parents, raw, uniq, kept) / elapsed / 1e9, 2),
         'cpu_baseline': None,
     }
+    if dom == 'ms_expand':
+        # the bound that actually binds k_expand: random 128-B line touches — one probe
+        # load per raw child, a CAS + atomicMin per new key (= per survivor), lost marks not counted
+        # (a lower bound) — against the measured random 16-B load rate over a 32 GiB table
+        touches = (raw + 2 * uniq) / len(per)
+        out['roofline']['random_access'] = {
+            'touches_per_launch': int(touches), 'achieved_G_per_s': round(touches / (ms_dom * 1e-3) / 1e9, 2),
+            'peak_G_per_s': RANDOM_LOAD_PEAK_G, 'frac': round(touches / (ms_dom * 1e-3) / 1e9 / RANDOM_LOAD_PEAK_G, 3),
+            'peak_source': 'profiles/micro/r1_randaccess.txt (load16, 32 GiB table)'}
     tr, tns, src = pmc_traffic(dom.replace('ms_', 'k_'))
     if tr is not None:
         out['roofline']['traffic'] = int(tr)
