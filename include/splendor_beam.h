@@ -54,7 +54,10 @@ typedef struct {
     int32_t device;            /* HIP device ordinal */
     int64_t beam_width;        /* State.solve(beam_width)              src/solver.py:396 */
     int32_t visited_log2;      /* log2 visited-set capacity (entries); 0 = auto from beam_width */
-    int32_t flags;             /* bit 0: collect per-kernel timings; bit 1: sharded (sbd_*) mode even at world_size 1 */
+    int32_t flags;             /* bit 0: collect per-kernel timings; bit 1: sharded (sbd_*) mode even at world_size 1;
+                                  bit 2 (test): generic first select pass instead of the one folded into the
+                                  emission; bit 3 (test): folded pass with its window forced off the keys
+                                  (exercises its fallback) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;

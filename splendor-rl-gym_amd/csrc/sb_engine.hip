@@ -860,14 +860,19 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     if (!heur) {
         hipLaunchKernelGGL(EMIT_K(-1), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, E.lost.p,
                            E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase, 0u,
-                           E.d_small + 1, (unsigned long long*)nullptr);
+                           E.d_small + 1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                           (const uint64_t*)nullptr);
     } else {
-        unsigned long long* krange = topk_range_reset(E.topk, E.s);
+        const bool fused = !(E.cfg.flags & 4);
+        unsigned long long* krange = topk_range_reset(E.topk, E.s, fused, (E.cfg.flags & 8) != 0);
+        unsigned long long* fh = topk_fused_hist(E.topk);
+        const uint64_t* fb = topk_fused_base(E.topk);
+        const unsigned egf = grid_cap(n, 256, 2048);   // fewer blocks: one histogram flush per block
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
-    hipLaunchKernelGGL((k_emit_w<H, false>), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, \
+    hipLaunchKernelGGL((k_emit_w<H, false>), dim3(egf), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, \
                        E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
-                       rbase, 0u, E.d_small + 1, krange);                                                         \
+                       rbase, 0u, E.d_small + 1, krange, fh, fb);                                                 \
     break;
             case 1: EMIT(1)
             case 2: EMIT(2)
@@ -884,7 +889,8 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     uint32_t* idx = nullptr;
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
-        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true, E.d_small + 1);
+        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true, E.d_small + 1,
+                             /*fused=*/!(E.cfg.flags & 4));
         idx = E.kidx.p;
     }
     if (timing) SB_HIP(hipEventRecord(ev[5], E.s));

@@ -107,9 +107,13 @@ struct TopkScratch {
 // range_ready: the producer of the keys already folded their min/max into the pair returned by
 // topk_range_reset (called before it ran on the same stream).  err (device word): bit 4 is set if the
 // sort's look-back wait hit its spin bound (reported by check_err_word; never expected).
+// fused: the producer also added every key to the first-pass histogram (topk_fused_hist/_base; keys
+// are IEEE images of positive doubles), which replaces the generic first select pass when usable.
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready = false, uint32_t* err = nullptr);
-unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st);
+                         hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false);
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false);
+unsigned long long* topk_fused_hist(TopkScratch& s);
+const uint64_t* topk_fused_base(TopkScratch& s);
 // size the scratch for n keys and keep kept (avoids allocation on the step path)
 void topk_reserve(TopkScratch& s, int64_t n, int64_t keep);
 

@@ -40,21 +40,24 @@ enum : int {
     ST_BASE2,   // output offset of group 2 (= A)
     ST_BASE3,   // output offset of group 3 (= A + G2)
     ST_TOPK,    // sort: bits [0, TOPK) vary among the kept keys
+    ST_FBASE,   // fused first pass: histogram bin b counts keys with key >> 47 == FBASE + b (edges clamped)
+    ST_FALLBACK,  // fused first pass unusable (threshold in a clamped bin): run the generic first pass
     ST_HIST = 16,
     ST_WORDS = ST_HIST + SEL_BINS
 };
 
 __device__ __forceinline__ uint64_t hi_bits(uint64_t k, uint64_t sh) { return sh >= 64 ? 0ull : k >> sh; }
 
-__global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range) {
+__global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range, int fused) {
     const int t = threadIdx.x;
-    if (t < ST_HIST && (t > ST_MAX || !keep_range)) st[t] = 0;
+    if (t < ST_HIST && (t > ST_MAX || !keep_range) && !(fused && t == ST_FBASE)) st[t] = 0;
     __syncthreads();
     if (t == 0) {
         if (!keep_range) st[ST_MIN] = ~0ull;
         st[ST_NEED] = (uint64_t)keep;
     }
-    for (int i = t; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
+    if (!fused)
+        for (int i = t; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
 }
 
 __global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
@@ -80,7 +83,8 @@ __global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict_
 }
 
 // common high bits of all keys: SH = position above the highest differing bit
-__global__ void k_tk_setup(uint64_t* st) {
+__global__ void k_tk_setup(uint64_t* st, int only_fallback) {
+    if (only_fallback && !st[ST_FALLBACK]) return;
     const uint64_t x = st[ST_MIN] ^ st[ST_MAX];
     const uint64_t top = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
     st[ST_SH] = top;
@@ -90,8 +94,8 @@ __global__ void k_tk_setup(uint64_t* st) {
 
 // histogram of the next digit over the elements matching the resolved prefix; n from n_dev if given
 __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
-                                                   const uint64_t* __restrict__ n_dev, uint64_t* st) {
-    if (st[ST_DONE]) return;
+                                                   const uint64_t* __restrict__ n_dev, uint64_t* st, int only_fallback) {
+    if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
     __shared__ uint32_t h[TK_NT / 64][SEL_BINS];
     const int w = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < (TK_NT / 64) * SEL_BINS; i += TK_NT) (&h[0][0])[i] = 0;
@@ -132,8 +136,8 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
 }
 
 // pick the bucket holding the need-th largest matching element; clears the histogram
-__global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st) {
-    if (st[ST_DONE]) return;
+__global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallback) {
+    if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
     __shared__ uint32_t lds[TK_NT / 64 + 1];
     const int t = threadIdx.x;
     const uint64_t sh = st[ST_SH];
@@ -165,6 +169,42 @@ __global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st) {
         }
         cum += c[j];
     }
+    for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
+}
+
+// First pass from the histogram the emission folded (bins of key >> 47 in [FBASE, FBASE + 2048), the
+// edge bins clamped): pick the bin holding the keep-th largest key.  An edge bin mixes prefixes, so a
+// threshold there (or a count that is not n) sets FALLBACK and the generic first pass runs instead.
+__global__ __launch_bounds__(TK_NT) void k_tk_pick_fused(uint64_t* st, int64_t n) {
+    __shared__ uint32_t lds[TK_NT / 64 + 1];
+    const int t = threadIdx.x;
+    constexpr int PER = SEL_BINS / TK_NT;
+    uint64_t c[PER];
+    uint64_t loc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        c[j] = st[ST_HIST + SEL_BINS - 1 - (t * PER + j)];
+        loc += c[j];
+    }
+    uint32_t tot;
+    uint64_t cum = block_excl_scan<TK_NT>((uint32_t)loc, lds, &tot);
+    const uint64_t need = st[ST_NEED];
+    if (t == 0) st[ST_FALLBACK] = 1;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int b = SEL_BINS - 1 - (t * PER + j);
+        if (c[j] && cum < need && cum + c[j] >= need && (int64_t)tot == n && b > 0 && b < SEL_BINS - 1) {
+            const uint64_t nneed = need - cum;
+            st[ST_NEED] = nneed;
+            st[ST_PREFIX] = st[ST_FBASE] + (uint64_t)b;
+            st[ST_SH] = 47;
+            st[ST_DONE] = c[j] == nneed;
+            st[ST_FALLBACK] = 0;
+        }
+        cum += c[j];
+    }
+    __syncthreads();
     for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
 }
 
@@ -517,9 +557,20 @@ void TopkScratch::release() {
     small.release();
 }
 
-__global__ void k_tk_range_reset(uint64_t* st) {
-    st[ST_MIN] = ~0ull;
-    st[ST_MAX] = 0;
+// before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
+// first-pass window (from the previous turn's maximum: its top bin sits 64 bins (two binades) above
+// it) and zero the histogram the producer adds to
+__global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window) {
+    if (threadIdx.x == 0) {
+        if (fused) {
+            const int64_t top = (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
+            st[ST_FBASE] = off_window ? 0 : (top < 0 ? 0 : (uint64_t)top);
+        }
+        st[ST_MIN] = ~0ull;
+        st[ST_MAX] = 0;
+    }
+    if (fused)
+        for (int i = threadIdx.x; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
 }
 
 void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
@@ -536,14 +587,17 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     s.small.ensure(ST_WORDS);
 }
 
-unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st) {
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window) {
     s.small.ensure(ST_WORDS);
-    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(1), 0, st, s.small.p);
+    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(256), 0, st, s.small.p, (int)fused, (int)off_window);
     return (unsigned long long*)(s.small.p + ST_MIN);
 }
 
+unsigned long long* topk_fused_hist(TopkScratch& s) { return (unsigned long long*)(s.small.p + ST_HIST); }
+const uint64_t* topk_fused_base(TopkScratch& s) { return s.small.p + ST_FBASE; }
+
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready, uint32_t* err) {
+                         hipStream_t st, bool range_ready, uint32_t* err, bool fused) {
     if (n <= 0 || keep <= 0) return 0;
     const int64_t m = n < keep ? n : keep;
     s.k0.ensure(m);
@@ -552,7 +606,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.v1.ensure(m);
     s.small.ensure(ST_WORDS);
     uint64_t* stv = s.small.p;
-    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m, (int)range_ready);
+    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m, (int)range_ready, (int)fused);
     if (!range_ready)
         hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
     const bool selected = n > keep;
@@ -563,10 +617,12 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         s.ck.ensure(n);
         s.ci.ensure(n);
         const unsigned hg = grid_for(n, TK_NT * 16, 2048);
-        hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv);
-        // first digit over all keys, then partition: above -> output group 1, bucket -> candidates
-        hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv);
-        hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv);
+        // first digit over all keys (folded into the producer when fused, generic pass as fallback),
+        // then partition: above -> output group 1, bucket -> candidates
+        if (fused) hipLaunchKernelGGL(k_tk_pick_fused, dim3(1), dim3(TK_NT), 0, st, stv, n);
+        hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv, (int)fused);
+        hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, (int)fused);
+        hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, (int)fused);
         hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
                            stv, s.tile_a.p, s.tile_b.p);
         hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv, (int)ST_A,
@@ -578,8 +634,8 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         // remaining digits on the candidates (device-side count; passes after DONE exit at once)
         const uint64_t* nc = stv + ST_NC;
         for (int pass = 0; pass < SEL_PASSES_C; pass++) {
-            hipLaunchKernelGGL(k_tk_hist, dim3(std::min(hg, 512u)), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv);
-            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv);
+            hipLaunchKernelGGL(k_tk_hist, dim3(std::min(hg, 512u)), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, 0);
+            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
         }
         // candidates above T -> group 2, the first NEED ties -> group 3
         hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p,

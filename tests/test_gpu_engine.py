@@ -129,11 +129,11 @@ def test_device_topk_key_ranges():
 
 
 # ---------------------------------------------------------------- whole solves
-def _run_pair(goal, heur, width, seed, use_heuristic=True):
+def _run_pair(goal, heur, width, seed, use_heuristic=True, test_flags=0):
     from splendor_amd.engine import HEURISTIC_IDS
     st = _mt(seed)
     eng = BeamEngine(goal_pts=goal, use_heuristic=use_heuristic, heuristic=HEURISTIC_IDS.get(heur, 0),
-                     beam_width=width, mt_state625=st)
+                     beam_width=width, mt_state625=st, test_flags=test_flags)
     return eng, st
 
 
@@ -142,8 +142,8 @@ def _skey(lo, hi):
     return codec.to_signed(codec.state_key(cards, gems))
 
 
-def _check_against_golden(g):
-    eng, _ = _run_pair(g['goal'], g['heuristic'], g['beam_width'], g['seed'])
+def _check_against_golden(g, test_flags=0):
+    eng, _ = _run_pair(g['goal'], g['heuristic'], g['beam_width'], g['seed'], test_flags=test_flags)
     turns = [t for t in g['turns'] if t['n_unique'] > 0]
     t = 0
     while True:
@@ -174,6 +174,16 @@ def test_solve_w300k_golden(name):
     if not golden_exists(name):
         pytest.skip(f'{name} not captured')
     _check_against_golden(golden(name))
+
+
+@pytest.mark.parametrize('flags', [4, 8])
+def test_solve_select_paths_golden(flags):
+    """The top-k's first select pass three ways: folded into the emission (every other solve test), the
+    generic pass (flags bit 2), and the folded pass with its window forced off the keys so that its
+    fallback runs (bit 3) — same beams every turn."""
+    _check_against_golden(golden('solve_g15_efficiency_w300000_s0.json'), test_flags=flags)
+    for g in golden('solves_small.json')[:6]:
+        _check_against_golden(g, test_flags=flags)
 
 
 def test_solve_c3_w4m_oracle_golden():
