@@ -42,6 +42,7 @@ enum : int {
     ST_TOPK,    // sort: bits [0, TOPK) vary among the kept keys
     ST_FBASE,   // fused first pass: histogram bin b counts keys with key >> 47 == FBASE + b (edges clamped)
     ST_FALLBACK,  // fused first pass unusable (threshold in a clamped bin): run the generic first pass
+    ST_SLO,     // sort: lowest possible kept key; digits are taken from key - SLO
     ST_HIST = 16,
     ST_WORDS = ST_HIST + SEL_BINS
 };
@@ -342,15 +343,18 @@ __global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64
 }
 
 // bits that vary among the kept keys: [lowest kept, max]; lowest kept >= prefix << sh
+// The kept keys lie in [lo, max]: sorting key - lo (same order) needs only the bits of max - lo,
+// one digit fewer than the bits in which lo and max differ when the range crosses a power of two.
 __global__ void k_tk_sortsetup(uint64_t* st, int selected) {
     uint64_t lo = st[ST_MIN];
     if (selected) lo = st[ST_SH] >= 64 ? 0ull : (st[ST_PREFIX] << st[ST_SH]);
-    const uint64_t x = lo ^ st[ST_MAX];
+    const uint64_t x = st[ST_MAX] - lo;
+    st[ST_SLO] = lo;
     st[ST_TOPK] = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
 }
 
 // ---- stable LSD radix sort of the kept set, one kernel per 8-bit digit (decoupled look-back)
-// Digit p of key k is (~k >> 8p) & 255 (ascending digits = descending keys).  k_os_hist builds the
+// Digit p of key k is (~(k - SLO) >> 8p) & 255 (ascending digits = descending keys).  k_os_hist builds the
 // global histograms of every needed digit in one read.  Pass p: tiles of OS_TILE elements take
 // tickets in launch order; a tile ranks its elements stably ((round, wave) counts per digit + the
 // lane rank from a wave match), publishes its per-digit counts, looks back over its predecessors'
@@ -387,6 +391,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
                                                    const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     __shared__ uint32_t h[8][256];
     const int P = sort_passes(st);
+    const uint64_t slo = st[ST_SLO];
     for (int i = threadIdx.x; i < 8 * 256; i += OS_NT) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t lt = lanemask_lt();
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
     for (int64_t i0 = (int64_t)blockIdx.x * OS_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
         uint64_t kk[OS_IPT];
 #pragma unroll
-        for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~keys[i0 + r * stride] : 0ull;
+        for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~(keys[i0 + r * stride] - slo) : 0ull;
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const bool valid = i0 + r * stride < n;
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     const int64_t tile = s_tile;
     const int64_t base = tile * OS_TILE;
     const int shift = 8 * p;
+    const uint64_t slo = st[ST_SLO];
     const uint64_t lt = lanemask_lt();
     uint64_t kk[OS_IPT];
     uint32_t vv[OS_IPT];
@@ -456,7 +462,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     for (int r = 0; r < OS_IPT; r++) {
         const int64_t i = base + (int64_t)r * OS_NT + t;
         const bool valid = i < n;
-        const uint32_t d = (uint32_t)(((~kk[r]) >> shift) & 255);
+        const uint32_t d = (uint32_t)(((~(kk[r] - slo)) >> shift) & 255);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
