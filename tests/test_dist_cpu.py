@@ -1,4 +1,4 @@
-"""Sharded multi-rank protocol (splendor_amd.dist) on CPU with gloo, world sizes 2 and 3.
+"""Sharded multi-rank protocol (splendor_amd.dist) on CPU with gloo, world sizes 2, 3, 4 and 8.
 
 Every rank runs DistSolve over the Python reference backend; the concatenated rank slices of every
 turn must equal the single-process oracle's queue (keys, parent links), and the path and final MT
@@ -70,6 +70,9 @@ CASES = [
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False}),
     # key exchange in 3 chunks (claims in chunk order, displacements across chunks)
     (2, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'chunks': 3}),
+    # the driver's scaling runs use 4 and 8 ranks
+    (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'chunks': 2}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True}),
 ]
 
 

@@ -73,6 +73,8 @@ CASES = [
     (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1}),
     # key exchange in 3 chunks (claims in chunk order, displacements across chunks)
     (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3}),
+    # four ranks on the one GPU (the driver's scaling runs use 2, 4 and 8 GPUs)
+    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'chunks': 2}),
 ]
 
 
