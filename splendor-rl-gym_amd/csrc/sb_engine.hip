@@ -701,6 +701,31 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
 // Step buffers sized up front for a saturated beam (about 12.5 unique children per parent at most on
 // the goal-15 trajectories; DBuf grows past that if ever needed): a hipMalloc/hipFree on the step
 // path would serialise against in-flight work.
+// Sharded mode: the per-rank buffers of a saturated step sized up front from the local share of the
+// beam (records ≈ b_raw ≤ 32 per parent, survivors ≤ 14 per parent, 25% slack for uneven owners),
+// so that no hipMalloc lands in a timed step.
+static void preallocate_dist(Engine& E) {
+    const size_t wl = (size_t)(E.cfg.beam_width / std::max(1, (int)E.cfg.world_size) + 1) * 5 / 4;
+    const size_t nr = wl * 32, nu = wl * 14;
+    E.surv.ensure(wl * 3);
+    E.cnt.ensure(wl);
+    E.off.ensure(wl);
+    E.cand_key.ensure(nr);
+    E.cand_pos.ensure(nr);
+    E.digit.ensure(nr);
+    E.own_lost.ensure(nr / 64 + 1);
+    E.nlo.ensure(nu);
+    E.nhi.ensure(nu);
+    E.npar.ensure(nu);
+    E.skey.ensure(nu);
+    E.dsel_c.ensure(nu);
+    E.kidx.ensure(wl);
+    E.rkey.ensure(wl);
+    topk_reserve(E.topk, (int64_t)wl, (int64_t)wl);
+    E.scan.tiles.ensure(nr / SCAN_TILE + 1);
+    E.turn_mem.reserve(wl * 20 * 24);
+}
+
 static void preallocate(Engine& E) {
     const size_t W = (size_t)E.cfg.beam_width, nu = W * 14;
     E.cand.ensure(W * 3);
@@ -1090,6 +1115,8 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         noise_init(E.noise, mt_state625, ring, twists, E.s);
         if (distm && cfg->use_heuristic) noise_shard_setup(E.noise, cfg->rank, cfg->world_size, E.s);
         if (!distm && cfg->use_heuristic && cfg->beam_width <= (1ll << 24)) preallocate(E);
+        if (distm && cfg->use_heuristic && cfg->beam_width / std::max(1, (int)cfg->world_size) <= (1ll << 24))
+            preallocate_dist(E);
         SB_HIP(hipStreamSynchronize(E.s));
         return SB_OK;
     });
