@@ -219,7 +219,9 @@ int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);
 int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
 
 /* ---- realistic multi-player mode (MultiPlayerState, src/solver.py:471-860; config C4) ----
- * params = {players (2..4), target_points, len tier1, len tier2, len tier3}; tiers = 3 x 40 int32
+ * params = {players (2..4), target_points, len tier1, len tier2, len tier3, infinite_resources (0/1:
+ * GameConfig.infinite_resources, src/solver.py:33; 1 = speedrun takes, unlimited pool kept in w[11])};
+ * tiers = 3 x 40 int32
  * card orders of the tiers (visible first 4, then the deck, src/solver.py:94-119); root_w = the
  * 12-word packed root (oracle/csrc/oracle.c realistic section).  sb_destroy / sb_get_mt_state /
  * sb_num_turns / sb_turn_size / sb_sync / sb_visited_size accept realistic handles. */

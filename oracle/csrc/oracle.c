@@ -524,12 +524,18 @@ uint64_t oc_visited_size(oc_handle* h) { return h->visited.n; }
  *   w[8]  pool 3 bits x5 (0..14) | cp 15..16 | frt 17 | frp 18..20 (7 = None) | deck pointers 6 bits
  *         x3 (21..38) | visible counts 3 bits x3 (39..47)
  *   w[9]  tier-1 visible 4 x 7 bits (0..27), tier-2 visible (28..55);  w[10] tier-3 visible (0..27)
+ *   w[11] infinite_resources=True only: pool 12 bits x5 (it grows by the gems paid for cards; the
+ *         3-bit pool field of w[8] is then 0)
+ * infinite_resources=True (:635-659): takes are the speedrun take table of the current player's gems
+ * (get_takes()[gems], the pool untouched); buys as above (the pool grows by the gems paid).
  */
 #define RW 12
-typedef struct { int P, target; int tier[3][40]; int tlen[3]; } rgame_t;
+typedef struct { int P, target; int tier[3][40]; int tlen[3]; int inf; } rgame_t;
 typedef struct { uint64_t w[RW]; } rst_t;
 
-static inline int r_pool(const rst_t* s, int c) { return (int)((s->w[8] >> (3 * c)) & 7); }
+static inline int r_pool(const rgame_t* G, const rst_t* s, int c) {
+    return G->inf ? (int)((s->w[11] >> (12 * c)) & 4095) : (int)((s->w[8] >> (3 * c)) & 7);
+}
 static inline int r_cp(const rst_t* s) { return (int)((s->w[8] >> 15) & 3); }
 static inline int r_frt(const rst_t* s) { return (int)((s->w[8] >> 17) & 1); }
 static inline int r_frp(const rst_t* s) { int v = (int)((s->w[8] >> 18) & 7); return v == 7 ? -1 : v; }
@@ -542,10 +548,16 @@ static inline int r_vis(const rst_t* s, int t, int j) {
 static inline st_t r_player(const rst_t* s, int i) { st_t p = {s->w[2 * i], s->w[2 * i + 1]}; return p; }
 static inline void r_set_player(rst_t* s, int i, st_t p) { s->w[2 * i] = p.lo; s->w[2 * i + 1] = p.hi; }
 
-static void r_set_meta(rst_t* s, const int pool[5], int cp, int frt, int frp, const int dptr[3], const int nvis[3],
-                       const int vis[3][4]) {
+static void r_set_meta(const rgame_t* G, rst_t* s, const int pool[5], int cp, int frt, int frp, const int dptr[3],
+                       const int nvis[3], const int vis[3][4]) {
     uint64_t m = 0;
-    for (int c = 0; c < 5; c++) m |= (uint64_t)pool[c] << (3 * c);
+    if (G->inf) {
+        uint64_t w11 = 0;
+        for (int c = 0; c < 5; c++) w11 |= (uint64_t)pool[c] << (12 * c);
+        s->w[11] = w11;
+    } else {
+        for (int c = 0; c < 5; c++) m |= (uint64_t)pool[c] << (3 * c);
+    }
     m |= (uint64_t)cp << 15;
     m |= (uint64_t)(frt ? 1 : 0) << 17;
     m |= (uint64_t)(frp < 0 ? 7 : frp) << 18;
@@ -583,7 +595,7 @@ static uint64_t r_key(const rgame_t* G, const rst_t* s) {
         hp[i] = th_tuple(f, 6);
     }
     uint64_t lp[5], lv[12];
-    for (int c = 0; c < 5; c++) lp[c] = (uint64_t)r_pool(s, c);
+    for (int c = 0; c < 5; c++) lp[c] = (uint64_t)r_pool(G, s, c);
     int nv = 0;
     for (int t = 0; t < 3; t++)
         for (int j = 0; j < r_nvis(s, t); j++) lv[nv++] = (uint64_t)r_vis(s, t, j);
@@ -599,8 +611,8 @@ static int r_can_afford(st_t p, int c) {
     return 1;
 }
 
-static void r_unpack_meta(const rst_t* s, int pool[5], int dptr[3], int nvis[3], int vis[3][4]) {
-    for (int c = 0; c < 5; c++) pool[c] = r_pool(s, c);
+static void r_unpack_meta(const rgame_t* G, const rst_t* s, int pool[5], int dptr[3], int nvis[3], int vis[3][4]) {
+    for (int c = 0; c < 5; c++) pool[c] = r_pool(G, s, c);
     for (int t = 0; t < 3; t++) {
         dptr[t] = r_dptr(s, t);
         nvis[t] = r_nvis(s, t);
@@ -611,7 +623,7 @@ static void r_unpack_meta(const rst_t* s, int pool[5], int dptr[3], int nvis[3],
 static int r_successors(const rgame_t* G, const rst_t* s, rst_t* out) {
     const int cur = r_cp(s), nxt = (cur + 1) % G->P, frt = r_frt(s), frp = r_frp(s);
     int pool[5], dptr[3], nvis[3], vis[3][4];
-    r_unpack_meta(s, pool, dptr, nvis, vis);
+    r_unpack_meta(G, s, pool, dptr, nvis, vis);
     st_t me = r_player(s, cur);
     int g[NCOL], b[NCOL];
     for (int c = 0; c < NCOL; c++) g[c] = st_gem(me, c);
@@ -641,9 +653,27 @@ static int r_successors(const rgame_t* G, const rst_t* s, rst_t* out) {
             const int frp2 = frt ? frp : (frt2 ? cur : -1);
             rst_t c2 = *s;
             r_set_player(&c2, cur, pl);
-            r_set_meta(&c2, np, nxt, frt2, frp2, dp2, nv2, vis2);
+            r_set_meta(G, &c2, np, nxt, frt2, frp2, dp2, nv2, vis2);
             out[n++] = c2;
         }
+    if (G->inf) {                                 /* speedrun take table, pool untouched (:635-659) */
+        const int tot = g[0] + g[1] + g[2] + g[3] + g[4];
+        if (tot <= 10) {
+            const int bk = tot <= 7 ? 0 : tot - 7;
+            for (int k = 0; k < NPATS[bk]; k++) {
+                const pat_t* p = &PATS[bk][k];
+                if (p->two_at >= 0 && g[p->two_at] > MAXG - 4) continue;
+                int ng[NCOL], ok = 1;
+                for (int i = 0; i < NCOL; i++) { ng[i] = g[i] + p->d[i]; if (ng[i] < 0 || ng[i] > MAXG) ok = 0; }
+                if (!ok) continue;
+                rst_t c2 = *s;
+                r_set_player(&c2, cur, st_make(me.lo, me.hi, ng, st_pts(me), st_saved(me)));
+                r_set_meta(G, &c2, pool, nxt, frt, frp, dptr, nvis, vis);
+                out[n++] = c2;
+            }
+        }
+        return n;
+    }
     int avail[5], na = 0, tot = 0;
     for (int c = 0; c < 5; c++) { if (pool[c] > 0) avail[na++] = c; tot += g[c]; }
     for (int x = 0; x < na; x++)                  /* combinations(available, 3) */
@@ -656,7 +686,7 @@ static int r_successors(const rgame_t* G, const rst_t* s, rst_t* out) {
                 for (int k = 0; k < 3; k++) { ng[cs[k]]++; np[cs[k]]--; }
                 rst_t c2 = *s;
                 r_set_player(&c2, cur, st_make(me.lo, me.hi, ng, st_pts(me), st_saved(me)));
-                r_set_meta(&c2, np, nxt, frt, frp, dptr, nvis, vis);
+                r_set_meta(G, &c2, np, nxt, frt, frp, dptr, nvis, vis);
                 out[n++] = c2;
             }
     for (int x = 0; x < na; x++) {                /* two of one colour */
@@ -667,7 +697,7 @@ static int r_successors(const rgame_t* G, const rst_t* s, rst_t* out) {
         ng[c0] += 2; np[c0] -= 2;
         rst_t c2 = *s;
         r_set_player(&c2, cur, st_make(me.lo, me.hi, ng, st_pts(me), st_saved(me)));
-        r_set_meta(&c2, np, nxt, frt, frp, dptr, nvis, vis);
+        r_set_meta(G, &c2, np, nxt, frt, frp, dptr, nvis, vis);
         out[n++] = c2;
     }
     return n;
@@ -713,8 +743,9 @@ static inline uint64_t f64_key(double d) {
 }
 
 /* ---- ctypes surface for tests */
+/* params: [players, target, tier lengths x3, infinite_resources] */
 static int r_load_game(rgame_t* G, const int32_t* params, const int32_t* tiers) {
-    G->P = params[0]; G->target = params[1];
+    G->P = params[0]; G->target = params[1]; G->inf = params[5] != 0;
     for (int t = 0; t < 3; t++) { G->tlen[t] = params[2 + t]; for (int k = 0; k < G->tlen[t]; k++) G->tier[t][k] = tiers[t * 40 + k]; }
     return (G->P >= 2 && G->P <= 4) ? 0 : -1;
 }
@@ -728,7 +759,7 @@ uint64_t ort_key(const int32_t* params, const int32_t* tiers, const uint64_t* w)
 int ort_successors(const int32_t* params, const int32_t* tiers, const uint64_t* w, uint64_t* out, uint64_t* keys) {
     rgame_t G; r_load_game(&G, params, tiers);
     rst_t s; memcpy(s.w, w, sizeof s.w);
-    rst_t kids[64];
+    rst_t kids[128];
     int n = r_successors(&G, &s, kids);
     for (int k = 0; k < n; k++) { memcpy(out + k * RW, kids[k].w, sizeof kids[k].w); keys[k] = r_key(&G, &kids[k]); }
     return n;
@@ -809,7 +840,7 @@ int ort_step(ort_handle* h, oc_stats* out) {
     int64_t cap = cur->n * 32 + 64, nq = 0, nraw = 0;
     rst_t* nxt = (rst_t*)malloc(sizeof(rst_t) * cap);
     uint32_t* npar = (uint32_t*)malloc(sizeof(uint32_t) * cap);
-    rst_t kids[64];
+    rst_t kids[128];
     for (int64_t r = 0; r < cur->n; r++) {
         int nk = r_successors(&h->G, &cur->st[r], kids);
         nraw += nk;

@@ -613,6 +613,7 @@ struct RGame {
     int P, target;
     int tlen[3];
     uint8_t tier[3][40];
+    int inf;   // infinite_resources=True: speedrun takes, pool in w[11] (sb_realistic.inc)
 };
 
 struct Turn {

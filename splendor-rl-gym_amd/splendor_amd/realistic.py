@@ -2,8 +2,10 @@
 
 ``GameConfig``, ``GemPool``, ``CardMarket``, ``PlayerState`` and ``MultiPlayerState`` keep the
 reference's fields, constructors, hashing and printing; ``MultiPlayerState.solve`` runs the beam
-search on the MI355X engine (``sbr_*`` entry points of libsplendor_beam.so, 2 players — the CLI's
-and config C4's case).  Packed device form: 12 x u64 per state (``include/splendor_beam.h``).
+search on the MI355X engine (``sbr_*`` entry points of libsplendor_beam.so; 2-4 players, the gem
+pool limited (the CLI's and config C4's case) or unlimited (``infinite_resources=True``, whose takes
+are the speedrun take table, src/solver.py:635-659)).  Packed device form: 12 x u64 per state
+(``include/splendor_beam.h``).
 """
 from __future__ import annotations
 
@@ -201,8 +203,13 @@ def pack_state(s: MultiPlayerState, tiers0) -> np.ndarray:
         lo, hi = _enc_player(p.cards, p.gems, p.pts, p.saved)
         w[2 * i], w[2 * i + 1] = lo, hi
     m = 0
-    for c, v in enumerate(s.gem_pool.available):
-        m |= v << (3 * c)
+    if s.config.infinite_resources:   # the pool grows by the gems paid: 12-bit fields in w[11]
+        if any(v < 0 or v > 4095 for v in s.gem_pool.available):
+            raise ValueError('gem pool outside the packed range')
+        w[11] = sum(v << (12 * c) for c, v in enumerate(s.gem_pool.available))
+    else:
+        for c, v in enumerate(s.gem_pool.available):
+            m |= v << (3 * c)
     m |= s.current_player << 15
     m |= (1 if s.final_round_triggered else 0) << 17
     m |= (7 if s.final_round_player is None else s.final_round_player) << 18
@@ -232,7 +239,10 @@ def unpack_state(w, config: GameConfig, tiers0, turn_number: int) -> MultiPlayer
         cards, bonus, gems, pts, saved = _dec_player(w[2 * i], w[2 * i + 1])
         players.append(PlayerState(i, cards, bonus, gems, pts, saved))
     m = w[8]
-    pool = tuple((m >> (3 * c)) & 7 for c in range(5))
+    if config.infinite_resources:
+        pool = tuple((w[11] >> (12 * c)) & 4095 for c in range(5))
+    else:
+        pool = tuple((m >> (3 * c)) & 7 for c in range(5))
     cp = (m >> 15) & 3
     frt = bool((m >> 17) & 1)
     frp = (m >> 18) & 7
@@ -249,8 +259,10 @@ def unpack_state(w, config: GameConfig, tiers0, turn_number: int) -> MultiPlayer
 
 
 def game_params(config: GameConfig, tiers0) -> tuple[np.ndarray, np.ndarray]:
-    """int32 params [P, target, len t1, len t2, len t3] and tiers [3 x 40] for the engine / oracle."""
-    params = np.array([config.num_players, config.target_points] + [len(t) for t in tiers0], dtype=np.int32)
+    """int32 params [P, target, len t1, len t2, len t3, infinite_resources] and tiers [3 x 40] for the
+    engine / oracle."""
+    params = np.array([config.num_players, config.target_points] + [len(t) for t in tiers0] +
+                      [1 if config.infinite_resources else 0], dtype=np.int32)
     tiers = np.zeros((3, 40), dtype=np.int32)
     for t in range(3):
         tiers[t, :len(tiers0[t])] = tiers0[t]

@@ -217,7 +217,7 @@ def _mp_key(st):
     return st.hash
 
 
-def _run_realistic(goal, width, seed, shuffle, players=2):
+def _run_realistic(goal, width, seed, shuffle, players=2, infinite=False):
     import src.solver as S
     trace = []
     real_sorted = sorted
@@ -233,7 +233,7 @@ def _run_realistic(goal, width, seed, shuffle, players=2):
 
     gems_per_color = {2: 4, 3: 5, 4: 7}.get(players, 4)
     config = S.GameConfig(num_players=players, target_points=goal, gems_per_color=gems_per_color,
-                          infinite_resources=False)
+                          infinite_resources=infinite)
     S.sorted = traced_sorted
     try:
         g = S.MultiPlayerState.newgame(config=config, shuffle_market=shuffle, seed=seed if shuffle else None)
@@ -246,6 +246,7 @@ def _run_realistic(goal, width, seed, shuffle, players=2):
     last = sol[-1]
     m = g.market
     return {'goal': goal, 'beam_width': width, 'seed': seed, 'shuffle': shuffle, 'players': players,
+            'infinite': infinite,
             'market': {'t1': list(m.tier1_visible) + list(m.tier1_deck),
                        't2': list(m.tier2_visible) + list(m.tier2_deck),
                        't3': list(m.tier3_visible) + list(m.tier3_deck)},
@@ -287,17 +288,18 @@ def _enc_mp(s):
             'game_over': s.is_game_over()}
 
 
-def cmd_realistic_succ(_args):
+def cmd_realistic_succ(args, infinite=False, walks=60, name='realistic_succ.json'):
     """Ordered successor lists + hashes + competitive scores for realistic states (buy-biased walks)."""
     import src.solver as S
     heur = _competitive_heuristic()
     out = []
-    rng = random.Random(3)
+    rng = random.Random(3 if not infinite else 13)
     for players in (2, 3, 4):
         gpc = {2: 4, 3: 5, 4: 7}[players]
-        for walk in range(60):
+        for walk in range(walks):
             target = rng.choice((3, 6, 15))
-            cfg = S.GameConfig(num_players=players, target_points=target, gems_per_color=gpc, infinite_resources=False)
+            cfg = S.GameConfig(num_players=players, target_points=target, gems_per_color=gpc,
+                               infinite_resources=infinite)
             st = S.MultiPlayerState.newgame(cfg, shuffle_market=bool(walk % 2), seed=walk)
             m = st.market
             depth = rng.randrange(1, 60)
@@ -315,12 +317,28 @@ def cmd_realistic_succ(_args):
                 random.seed(17)
                 scores.append(heur(k).hex())
             out.append({'players': players, 'target': target, 'shuffle': bool(walk % 2), 'seed': walk,
+                        'infinite': infinite,
                         'market0': {'t1': list(m.tier1_visible) + list(m.tier1_deck),
                                     't2': list(m.tier2_visible) + list(m.tier2_deck),
                                     't3': list(m.tier3_visible) + list(m.tier3_deck)},
                         'state': _enc_mp(st), 'children': [_enc_mp(k) for k in kids], 'scores_seed17': scores,
                         'winner': st.get_winner()})
-    _dump('realistic_succ.json', out)
+    _dump(name, out)
+
+
+def cmd_realistic_inf_succ(args):
+    """The same captures with infinite_resources=True (takes = the speedrun take table, src/solver.py:635-659)."""
+    cmd_realistic_succ(args, infinite=True, walks=20, name='realistic_inf_succ.json')
+
+
+def cmd_realistic_inf_small(_args):
+    out = []
+    for goal, width, seed, shuffle, players in [(5, 300, 1, False, 2), (6, 1000, 2, True, 2), (8, 2000, 3, True, 2),
+                                                  (4, 200, 4, False, 3), (3, 100, 6, True, 4)]:
+        r = _run_realistic(goal, width, seed, shuffle, players, infinite=True)
+        print(goal, width, seed, shuffle, players, r['moves'], r['wall_s'])
+        out.append(r)
+    _dump('realistic_inf_small.json', out)
 
 
 def cmd_realistic_small(_args):
@@ -341,6 +359,8 @@ def main():
     sub.add_parser('bfs')
     sub.add_parser('realistic_succ')
     sub.add_parser('realistic_small')
+    sub.add_parser('realistic_inf_succ')
+    sub.add_parser('realistic_inf_small')
     p = sub.add_parser('solve')
     p.add_argument('--goal', type=int, required=True)
     p.add_argument('--heur', required=True)
@@ -355,7 +375,8 @@ def main():
     args = ap.parse_args()
     {'tables': cmd_tables, 'solve': cmd_solve, 'solves_small': cmd_solves_small, 'bfs': cmd_bfs,
      'realistic': cmd_realistic, 'realistic_succ': cmd_realistic_succ,
-     'realistic_small': cmd_realistic_small}[args.cmd](args)
+     'realistic_small': cmd_realistic_small, 'realistic_inf_succ': cmd_realistic_inf_succ,
+     'realistic_inf_small': cmd_realistic_inf_small}[args.cmd](args)
 
 
 if __name__ == '__main__':

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 def _root(g):
     cfg = GameConfig(num_players=g['players'], target_points=g['goal'],
-                     gems_per_color={2: 4, 3: 5, 4: 7}[g['players']], infinite_resources=False)
+                     gems_per_color={2: 4, 3: 5, 4: 7}[g['players']], infinite_resources=g.get('infinite', False))
     return MultiPlayerState.newgame(cfg, shuffle_market=g['shuffle'], seed=g['seed'] if g['shuffle'] else None)
 
 
@@ -47,6 +47,12 @@ def test_realistic_small_golden():
         _check(g)
 
 
+def test_realistic_infinite_small_golden():
+    """infinite_resources=True (speedrun takes, the pool only grows, src/solver.py:635-659)."""
+    for g in golden('realistic_inf_small.json'):
+        _check(g)
+
+
 def test_realistic_readme_example_golden():
     _check(golden('realistic_g6_p2_fixed_w3000_s0.json'))
 
@@ -56,8 +62,10 @@ def test_realistic_goal15_w20k_golden():
 
 
 def test_realistic_vs_oracle_stepwise():
-    for goal, width, seed, shuffle, players in [(7, 4000, 11, True, 2), (5, 800, 12, False, 3), (4, 300, 13, True, 4)]:
-        g = {'players': players, 'goal': goal, 'shuffle': shuffle, 'seed': seed}
+    for goal, width, seed, shuffle, players, inf in [(7, 4000, 11, True, 2, False), (5, 800, 12, False, 3, False),
+                                                     (4, 300, 13, True, 4, False), (9, 20000, 14, True, 2, True),
+                                                     (6, 2000, 15, False, 3, True)]:
+        g = {'players': players, 'goal': goal, 'shuffle': shuffle, 'seed': seed, 'infinite': inf}
         root = _root(g)
         random.seed(seed)
         st = random.getstate()[1]

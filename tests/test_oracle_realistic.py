@@ -13,7 +13,7 @@ from splendor_amd.realistic import (CardMarket, GameConfig, GemPool, MultiPlayer
 def state_from_fixture(fx, st, tiers0, target):
     P = fx['players']
     cfg = GameConfig(num_players=P, target_points=target, gems_per_color={2: 4, 3: 5, 4: 7}[P],
-                     infinite_resources=False)
+                     infinite_resources=fx.get('infinite', False))
     players = tuple(PlayerState(p[0], tuple(p[1]), tuple(p[2]), tuple(p[3]), p[4], p[5]) for p in st['players'])
     decks = [tuple(tiers0[t][len(tiers0[t]) - st['decklen'][t]:]) for t in range(3)]
     market = CardMarket(tuple(st['vis'][0]), tuple(st['vis'][1]), tuple(st['vis'][2]), *decks)
@@ -25,9 +25,12 @@ def _tiers0(fx):
     return [fx['market0']['t1'], fx['market0']['t2'], fx['market0']['t3']]
 
 
-def test_realistic_successors_hashes_scores():
+@pytest.mark.parametrize('name,min_children', [('realistic_succ.json', 500), ('realistic_inf_succ.json', 1000)])
+def test_realistic_successors_hashes_scores(name, min_children):
+    """Ordered successors, hashes, game-over flags and competitive scores; the second fixture has
+    infinite_resources=True (speedrun takes, unlimited pool, src/solver.py:635-659)."""
     n_children = 0
-    for fx in golden('realistic_succ.json'):
+    for fx in golden(name):
         t0 = _tiers0(fx)
         s = state_from_fixture(fx, fx['state'], t0, fx['target'])
         assert s.hash == fx['state']['hash']          # host mirror hashes like the reference
@@ -46,12 +49,12 @@ def test_realistic_successors_hashes_scores():
         for c, sc in zip(exp, fx['scores_seed17']):
             assert oracle_c.rt_score(params, tiers, c, k).hex() == sc
         n_children += len(kids)
-    assert n_children > 500
+    assert n_children > min_children
 
 
 def _solve_fixture(g):
     cfg = GameConfig(num_players=g['players'], target_points=g['goal'],
-                     gems_per_color={2: 4, 3: 5, 4: 7}[g['players']], infinite_resources=False)
+                     gems_per_color={2: 4, 3: 5, 4: 7}[g['players']], infinite_resources=g.get('infinite', False))
     t0 = [g['market']['t1'], g['market']['t2'], g['market']['t3']]
     assert tuple(map(tuple, t0)) == tuple(map(tuple, tier_lists(g['shuffle'], g['seed'] if g['shuffle'] else None)))
     root = MultiPlayerState.newgame(cfg, shuffle_market=g['shuffle'], seed=g['seed'] if g['shuffle'] else None)
@@ -75,6 +78,12 @@ def _solve_fixture(g):
 
 def test_realistic_small_solves():
     for g in golden('realistic_small.json'):
+        _solve_fixture(g)
+
+
+def test_realistic_infinite_small_solves():
+    for g in golden('realistic_inf_small.json'):
+        assert g['infinite']
         _solve_fixture(g)
 
 
