@@ -8,9 +8,9 @@ export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_expand|k_count_lm|k_emit|k_tk_|k_sort|k_gather' \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_expand|k_count_lm|k_emit|k_tk_|k_os_|k_gather' \
     --output-format csv -d "$OUT/pmc_fetch" -o run -- \
     python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_expand|k_count_lm|k_emit|k_tk_|k_sort|k_gather' \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_expand|k_count_lm|k_emit|k_tk_|k_os_|k_gather' \
     --output-format csv -d "$OUT/pmc_write" -o run -- \
     python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > "$OUT/bench_write.json" 2> "$OUT/write.err"

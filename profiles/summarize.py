@@ -17,11 +17,12 @@ from collections import defaultdict
 
 # kernels launched once per step on the saturated path (k_expand: the last launches include the
 # pipelined expansion of the turn after the last timed one — one per step either way)
-PER_STEP = ['k_expand', 'k_count_lm', 'k_emit_w<1>', 'k_tk_count', 'k_tk_write', 'k_gather', 'k_copy_idx']
+PER_STEP = ['k_expand', 'k_count_lm', 'k_emit_w<1, false>', 'k_tk_count', 'k_tk_write', 'k_os_hist', 'k_os_pass',
+            'k_gather_d', 'k_copy_idx']
 
 
 def short(name):
-    m = re.match(r'(?:void )?(?:sb::)?([A-Za-z_0-9]+(?:<\d+>)?)', name)
+    m = re.match(r'(?:void )?(?:sb::)?([A-Za-z_0-9]+(?:<[^>]*>)?)', name)
     return m.group(1) if m else name[:40]
 
 
@@ -31,39 +32,50 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(os.path.join(a.dir, 'trace', 'run_kernel_trace.csv'))))
+    def load(path, counter=None):
+        """[(name, start, end, value)] in dispatch order (value = counter value for PMC files)."""
+        out = []
+        for r in csv.DictReader(open(path)):
+            if counter is not None and r['Counter_Name'] != counter:
+                continue
+            out.append((short(r['Kernel_Name']), int(r['Start_Timestamp']), int(r['End_Timestamp']),
+                        float(r['Counter_Value']) if counter else None))
+        out.sort(key=lambda x: x[1])
+        return out
+
+    def timed_window(recs):
+        """Dispatches of the timed turns: the expansion of the first timed turn is launched (pipelined)
+        inside the step before it, the expansion after the last timed turn inside the last timed step;
+        the timed turns' kernels lie between those two expansion starts."""
+        ex = [r for r in recs if r[0] == 'k_expand']
+        t0, t1 = ex[-a.steps - 1][1], ex[-1][1]
+        return [r for r in recs if t0 <= r[1] < t1]
+
+    rows = load(os.path.join(a.dir, 'trace', 'run_kernel_trace.csv'))
     by = defaultdict(list)
     for r in rows:
-        by[short(r['Kernel_Name'])].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+        by[r[0]].append(r[2] - r[1])
     kernels = {}
     for k, durs in by.items():
         kernels[k] = {'calls': len(durs), 'total_ns': sum(durs), 'avg_ns': sum(durs) / len(durs)}
-    # timed-step view of the per-step kernels
-    # k_expand of the turn after the last timed one is launched inside the last timed step (pipelined
-    # front half): the timed turns' expansions are the dispatches before it
-    # (the select partition kernels run twice per step)
-    def window(k, seq):
-        if k == 'k_expand':
-            return seq[-a.steps - 1:-1]
-        return seq[-2 * a.steps:] if k in ('k_tk_count', 'k_tk_write') else seq[-a.steps:]
-
+    win = defaultdict(list)
+    for r in timed_window(rows):
+        win[r[0]].append(r[2] - r[1])
     timed = {}
     for k in PER_STEP:
-        if k in by:
-            d = window(k, by[k])
-            timed[k] = {'launches': len(d), 'avg_ns': sum(d) / len(d)}
+        if k in win:
+            d = win[k]
+            timed[k] = {'launches': len(d), 'avg_ns': sum(d) / len(d), 'per_step_ns': sum(d) / a.steps}
     pmc = {}
     for kind, fn in (('FETCH_SIZE', 'pmc_fetch'), ('WRITE_SIZE', 'pmc_write')):
         p = os.path.join(a.dir, fn, 'run_counter_collection.csv')
         if not os.path.exists(p):
             continue
         vals = defaultdict(list)
-        for r in csv.DictReader(open(p)):
-            if r['Counter_Name'] == kind:
-                vals[short(r['Kernel_Name'])].append(float(r['Counter_Value']))
+        for r in timed_window(load(p, kind)):
+            vals[r[0]].append(r[3])
         for k, v in vals.items():
-            w = window(k, v)
-            pmc.setdefault(k, {})[kind + '_KiB_timed_avg'] = sum(w) / len(w)
+            pmc.setdefault(k, {})[kind + '_KiB_timed_avg'] = sum(v) / len(v)
     for k, v in pmc.items():
         if 'FETCH_SIZE_KiB_timed_avg' in v and 'WRITE_SIZE_KiB_timed_avg' in v:
             v['hbm_bytes_per_launch'] = (2 * v['FETCH_SIZE_KiB_timed_avg'] + v['WRITE_SIZE_KiB_timed_avg']) * 1024
