@@ -29,16 +29,21 @@ def main():
                 print('built', out)
     else:
         steps = sys.argv[sys.argv.index('--steps') + 1] if '--steps' in sys.argv else '8'
+        modes = ['single', 'sharded'] if '--dist' in sys.argv else ['single']   # sharded: SB_FORCE_DIST=1 (N=1)
         for f in sorted(os.listdir(VDIR)):
-            env = dict(os.environ, SPLENDOR_BEAM_LIB=os.path.join(VDIR, f))
-            r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--no-cpu-baseline', '--steps', steps],
-                               env=env, capture_output=True, text=True, timeout=300)
-            line = [l for l in r.stdout.splitlines() if l.startswith('{')]
-            if not line:
-                print(f, 'FAILED', r.stderr[-500:], flush=True)
-                break
-            d = json.loads(line[0])
-            print(f'{f:28s} {d["value"] / 1e6:8.1f} M/s  {d["ms_per_step"]:.3f} ms  {d["phases_ms"]}', flush=True)
+            for mode in modes:
+                env = dict(os.environ, SPLENDOR_BEAM_LIB=os.path.join(VDIR, f))
+                if mode == 'sharded':
+                    env['SB_FORCE_DIST'] = '1'
+                r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--no-cpu-baseline', '--steps',
+                                    steps], env=env, capture_output=True, text=True, timeout=300)
+                line = [l for l in r.stdout.splitlines() if l.startswith('{')]
+                if not line:
+                    print(f, mode, 'FAILED', r.stderr[-500:], flush=True)
+                    continue
+                d = json.loads(line[0])
+                print(f'{f:28s} {mode:8s} {d["value"] / 1e6:8.1f} M/s  {d["ms_per_step"]:.3f} ms  '
+                      f'{d.get("phases_ms", "")}', flush=True)
 
 
 if __name__ == '__main__':

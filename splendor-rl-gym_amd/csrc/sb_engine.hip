@@ -18,7 +18,8 @@
 //   top-k           stable descending sort + truncate (src/solver.py:452-456; sb_sort.hip)
 //   k_gather        the kept beam for the next turn + the per-pts first-rank table
 //
-// Visited set: open addressing over 16-byte entries {key, tag}; key = EMPTY marks a free slot.
+// Visited set: open addressing over 16-byte entries {key, tag}; tag = EMPTY marks a free slot (the tag is
+// claimed first, the key stored after: probe_insert).
 // The tag is (turn+1) << 40 | parent rank << 8 | ordinal; tag prefix 0 is the root's turn.
 #include <math.h>
 #include <stdio.h>
@@ -51,43 +52,105 @@ struct alignas(16) Entry {
 constexpr int MAX_PROBE = 4096;
 
 // ------------------------------------------------------------------ visited-set probe
+// Slot protocol (tag first): a free slot has tag == EMPTY.  An inserter claims the slot AND sets its tag
+// with one 64-bit CAS on the tag word, then stores the key (write-through to L2).  A reader that finds a
+// tag but no key yet (the inserter's store is in flight) reads the slot again on its next loop iteration;
+// the inserter never waits on anyone and its store precedes that re-read in the wave's instruction
+// stream, so the wait always ends (a spin inside one iteration could deadlock a wave whose own lane won).  A new key thus costs one CAS + one store instead of
+// a key CAS + a tag atomicMin (profiles/micro/r1_claimcost.txt: cas+st_sc1 12.1 G/s vs cas+amin 10.6 G/s
+// over a 32 GiB table).  -DSB_KEY_FIRST builds the previous protocol (key CAS, then atomicMin of the tag).
+//
+// probe_insert: returns 1 when this call inserted `key` (its tag is in place), 0 when the key was
+// found (slot h, tag *cur as read: stale reads only over-estimate, tags only decrease), -1 on overflow.
+// losing CAS attempts store here (see probe_insert); spread over 256 lines so they do not serialise
+__device__ unsigned long long g_claim_sink[4096];
+
+template <bool PRE>
+__device__ __forceinline__ int probe_insert(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
+                                            uint64_t tag, uint64_t& h, uint64_t& cur, uint32_t* err) {
+    h = mix64(key) & mask;
+    int wait = 0;
+    for (int probe = 0;;) {
+        if (!PRE || probe > 0 || wait > 0) ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);   // key and tag, one load
+        uint64_t k = ent.x, tg = ent.y;
+#ifndef SB_KEY_FIRST
+        if (tg == EMPTY) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&tab[h].tag, (unsigned long long)EMPTY,
+                                            (unsigned long long)tag);
+            const bool won = prev == EMPTY;
+            // every CAS attempt stores (a loser into the sink), so the winner's store cannot be sunk onto
+            // the loop's exit path: it is issued before any lane of this wave reads a slot again
+            __hip_atomic_store(won ? (unsigned long long*)&tab[h].key : &g_claim_sink[(h * 16) & 4095],
+                               (unsigned long long)key,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (won) return 1;
+            tg = prev;
+        }
+        if (k == EMPTY)
+            k = __hip_atomic_load((unsigned long long*)&tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == EMPTY) {   // tag claimed, the key store still in flight: read the slot again (no advance)
+            if (++wait > (1 << 24)) {
+                atomicOr(err, 1u);
+                return -1;
+            }
+            continue;
+        }
+        if (k == key) {
+            cur = tg;
+            return 0;
+        }
+#else
+        if (k == EMPTY) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
+                                            (unsigned long long)key);
+            if (prev == EMPTY) {
+                const uint64_t old = atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+                if (old == EMPTY) return 1;
+                cur = old;   // a same-turn duplicate set its tag between our CAS and atomicMin
+                return 0;
+            }
+            if (prev == key) {
+                cur = tab[h].tag;
+                return 0;
+            }
+            k = prev;
+        }
+        if (k == key) {
+            cur = tg;
+            return 0;
+        }
+#endif
+        h = (h + 1) & mask;
+        if (++probe > MAX_PROBE) {
+            atomicOr(err, 1u);
+            return -1;
+        }
+    }
+}
+
 // Claim with displacement marking (single-GPU speedrun path).  The winner of a key within a turn is
 // the smallest tag (parent rank, ordinal) — the reference's first occurrence in next_queue order.  A
 // claimant that lowers a same-turn tag marks the displaced holder in `lost`; one whose atomicMin finds
 // a smaller tag has lost itself.  Every duplicate is therefore resolved by exactly one of the two, and
 // once the grid drains the survivors are cand & ~lost — no second pass over the table.
-__device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t mask, uint64_t key, uint64_t tag,
-                                               unsigned long long* __restrict__ lost, uint32_t* err) {
-    uint64_t h = mix64(key) & mask;
-    uint64_t cur;   // the entry's tag; stale reads only over-estimate (tags only decrease)
-    for (int probe = 0;; probe++) {
-        const ulonglong2 ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);   // key and tag, one load
-        uint64_t k = ent.x;
-        if (k == EMPTY) {
-            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
-                                      (unsigned long long)key);
-            if (prev == EMPTY) {
-                cur = EMPTY;
-                break;
-            }
-            if (prev == key) {
-                cur = tab[h].tag;
-                break;
-            }
-            k = prev;
-        }
-        if (k == key) {
-            cur = ent.y;
-            break;
-        }
-        h = (h + 1) & mask;
-        if (probe >= MAX_PROBE) {
-            atomicOr(err, 1u);
-            return false;
-        }
-    }
-    if (cur != EMPTY && cur < tag) return false;
+template <bool PRE>
+__device__ __forceinline__ bool claim_lm(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
+                                         uint64_t tag, unsigned long long* __restrict__ lost, uint32_t* err) {
+    uint64_t h, cur = EMPTY;
+    const int r = probe_insert<PRE>(tab, mask, key, ent, tag, h, cur, err);
+#ifdef SB_CLAIM_STATS
+    // err[1] old-turn keys, err[2] inserted, err[3] same-turn early-out, err[4] lost at atomicMin, err[5] displaced
+    if (r == 1) atomicAdd(err + 2, 1u);
+    else if (r == 0 && cur < (tag & ~((1ull << 40) - 1))) atomicAdd(err + 1, 1u);
+    else if (r == 0 && cur < tag) atomicAdd(err + 3, 1u);
+#endif
+    if (r != 0) return r == 1;
+    if (cur < tag) return false;
     const uint64_t old = atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
+#ifdef SB_CLAIM_STATS
+    if (old < tag) atomicAdd(err + 4, 1u);
+    else atomicAdd(err + 5, 1u);
+#endif
     if (old < tag) return false;
     if (old != EMPTY) {   // old > tag >= this turn's prefix: a same-turn holder, now displaced
         const uint64_t ro = (old >> 8) & 0xFFFFFFFFull;
@@ -97,56 +160,15 @@ __device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t
     return true;
 }
 
+__device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t mask, uint64_t key, uint64_t tag,
+                                               unsigned long long* __restrict__ lost, uint32_t* err) {
+    return claim_lm<false>(tab, mask, key, make_ulonglong2(0, 0), tag, lost, err);
+}
+
 // visit_claim_lm with the entry at the key's home slot already loaded (ent)
 __device__ __forceinline__ bool visit_claim_lm_pre(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
                                                    uint64_t tag, unsigned long long* __restrict__ lost, uint32_t* err) {
-    uint64_t h = mix64(key) & mask;
-    uint64_t cur;
-    for (int probe = 0;; probe++) {
-        if (probe > 0) ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);
-        uint64_t k = ent.x;
-        if (k == EMPTY) {
-            uint64_t prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY,
-                                      (unsigned long long)key);
-            if (prev == EMPTY) {
-                cur = EMPTY;
-                break;
-            }
-            if (prev == key) {
-                cur = tab[h].tag;
-                break;
-            }
-            k = prev;
-        }
-        if (k == key) {
-            cur = ent.y;
-            break;
-        }
-        h = (h + 1) & mask;
-        if (probe >= MAX_PROBE) {
-            atomicOr(err, 1u);
-            return false;
-        }
-    }
-#ifdef SB_CLAIM_STATS
-    // err[1] old-turn keys, err[2] inserted, err[3] same-turn early-out, err[4] lost at atomicMin, err[5] displaced
-    if (cur != EMPTY && cur < (tag & ~((1ull << 40) - 1))) atomicAdd(err + 1, 1u);
-    else if (cur == EMPTY) atomicAdd(err + 2, 1u);
-    else if (cur < tag) atomicAdd(err + 3, 1u);
-#endif
-    if (cur != EMPTY && cur < tag) return false;
-    const uint64_t old = atomicMin((unsigned long long*)&tab[h].tag, (unsigned long long)tag);
-#ifdef SB_CLAIM_STATS
-    if (old < tag) atomicAdd(err + 4, 1u);
-    else if (old != EMPTY) atomicAdd(err + 5, 1u);
-#endif
-    if (old < tag) return false;
-    if (old != EMPTY) {
-        const uint64_t ro = (old >> 8) & 0xFFFFFFFFull;
-        const uint32_t oo = (uint32_t)(old & 255);
-        atomicOr(&lost[ro * 3 + (oo >> 6)], 1ull << (oo & 63));
-    }
-    return true;
+    return claim_lm<true>(tab, mask, key, ent, tag, lost, err);
 }
 
 __device__ __forceinline__ uint64_t lookup_tag(const Entry* __restrict__ tab, uint64_t mask, uint64_t key) {
