@@ -1131,6 +1131,12 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         // MT chunk = 256 producers x twists x 624 words ~ 16 draws per beam slot; ring >= 4 chunks
         int64_t twists = 1;
         while (twists < 4096 && (double)twists * 256 * 624 < (double)cfg->beam_width * 16) twists <<= 1;
+        if (distm) {   // sharded: one round (a chunk per rank) covers >= 2 steps (~12.5 W draws per step)
+            twists = 1;
+            while (twists < 4096 && (double)twists * 256 * 624 * std::max(1, (int)cfg->world_size) <
+                                        (double)cfg->beam_width * 64)
+                twists <<= 1;
+        }
         uint64_t ring = 1ull << 24;
         while ((ring < (uint64_t)cfg->beam_width * 64 || ring < 4ull * 256 * 624 * (uint64_t)twists) &&
                ring < (1ull << 35))

@@ -190,7 +190,10 @@ class ShardNoise:
     def prepare(self, A: int, N: int, all_n: np.ndarray):
         """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission."""
         c, b = self.c, self.b
-        if self.pending is not None:
+        # the round in flight is gathered only once its draws are needed (the same decision on every
+        # rank: gen_total and A + N are global), so its generation overlaps whole steps instead of the
+        # host waiting for it at the next turn
+        if self.pending is not None and self.gen_total < A + N:
             self._collect()
         while self.gen_total < A + N:
             self._launch()
@@ -216,8 +219,8 @@ class ShardNoise:
             wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv])
         b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
-        # next round in the background (side stream) while the step goes on; gathered next turn
-        if self.gen_total < A + N + 2 * N:
+        # next round in the background (side stream) while the steps go on; gathered when needed
+        if self.pending is None and self.gen_total < A + N + 4 * N:   # >= 3 steps to generate it
             self._launch()
 
 
