@@ -63,11 +63,17 @@ class Comm:
         dist.all_reduce(t, op=op)
         return t.cpu().numpy()
 
+    def _gather_flat(self, t: torch.Tensor) -> torch.Tensor:
+        """Every rank's equal-shape tensor, concatenated rank-major in one flat tensor: one collective
+        (all_gather_into_tensor), so the host reads it back with one copy instead of one per rank."""
+        s = self._to(t).reshape(-1)
+        out = torch.empty(self.world * s.numel(), dtype=s.dtype, device=s.device)
+        dist.all_gather_into_tensor(out, s)
+        return out
+
     def allgather_int(self, v: int) -> np.ndarray:
-        t = self._to(torch.tensor([int(v)], dtype=torch.int64, device=self.device))
-        out = [torch.zeros_like(t) for _ in range(self.world)]
-        dist.all_gather(out, t)
-        return np.array([int(x.item()) for x in out], dtype=np.int64)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
+        return self._gather_flat(t).cpu().numpy().astype(np.int64)
 
     def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
         send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
@@ -111,17 +117,13 @@ class Comm:
 
     def allgather_array(self, arr: np.ndarray) -> np.ndarray:
         """(world, len) int64 array of every rank's equal-length int vector."""
-        t = self._to(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device))
-        out = [torch.zeros_like(t) for _ in range(self.world)]
-        dist.all_gather(out, t)
-        return np.stack([x.cpu().numpy() for x in out])
+        a = np.ascontiguousarray(arr, dtype=np.int64)
+        t = torch.from_numpy(a).to(self.device)
+        return self._gather_flat(t).cpu().numpy().reshape(self.world, len(a))
 
-    def allgather_tensor(self, t: torch.Tensor) -> list[torch.Tensor]:
-        """Every rank's equal-shape tensor, on this rank's device."""
-        s = self._to(t)
-        out = [torch.empty_like(s) for _ in range(self.world)]
-        dist.all_gather(out, s)
-        return [self._back(x) for x in out]
+    def allgather_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """(world, *t.shape): every rank's equal-shape tensor, on this rank's device."""
+        return self._back(self._gather_flat(t).reshape((self.world,) + tuple(t.shape)))
 
     def broadcast_ints(self, vals, src: int) -> list[int]:
         t = self._to(torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device))
@@ -171,7 +173,7 @@ class ShardNoise:
         slot, counts = self.pending
         self.pending = None
         b.noise_sync()
-        allc = [x.cpu().numpy().astype(np.int64) for x in c.allgather_tensor(counts)]
+        allc = c.allgather_tensor(counts).cpu().numpy().astype(np.int64)   # (world, P*S)
         for r in range(c.world):   # chunk order: this round's chunk of rank 0, 1, ...
             cum = np.concatenate([[0], np.cumsum(allc[r])]).astype(np.int64)
             self.chunks.append((self.gen_total, cum, r, slot))
@@ -364,7 +366,7 @@ class DistSolve:
                 self._multiselect(pos, st)
                 self._mark(st, 'sel_passes')
                 if has_top:
-                    eq_all = torch.cat(c.allgather_tensor(b.sel_eq()))
+                    eq_all = c.allgather_tensor(b.sel_eq()).reshape(-1)
             self._mark(st, 'sel_eq')
             dest_counts = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
         else:
