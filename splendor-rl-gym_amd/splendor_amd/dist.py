@@ -243,7 +243,7 @@ class DistSolve:
         self._turn_sync()
         self.noise = ShardNoise(backend, comm) if use_heuristic else None
         self.consumed = 0                       # accepted draws used so far (global)
-        self.nchunk = int(os.environ.get('SB_DIST_CHUNKS', '4'))   # key exchange / claim pipeline depth
+        self.nchunk = int(os.environ.get('SB_DIST_CHUNKS', '8'))   # key exchange / claim pipeline depth
         self.chunk_min = int(os.environ.get('SB_DIST_CHUNK_MIN', str(1 << 23)))   # fewer raw records: one chunk
 
     def offset(self, turn=None) -> int:
