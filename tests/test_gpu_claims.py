@@ -1,0 +1,60 @@
+"""Visited-set claim protocol under contention (GPU, through the C-ABI sbd_owner_* entry points).
+
+The owner-side claim (csrc/sb_dist.inc claim_rec over probe_insert, csrc/sb_engine.hip) must settle
+every key to its first occurrence in record-index order — `if next_step in trail: continue` with
+first-occurrence order, src/solver.py:446-450 — however the claims interleave: heavy duplication
+(thousands of records per key, many lanes of one wave on one slot), long probe chains (table at
+~50% load) and chunks claimed out of index order (later chunks first, so earlier records displace
+holders and mark them lost).  Expected answers come from numpy: ret[i] = 1 iff i is the first index
+of keys[i].
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _backend(log2):
+    from splendor_amd.dist import HipBackend
+    random.seed(0)
+    return HipBackend(rank=0, world=1, device_index=0, goal_pts=15, use_heuristic=False, heuristic=0,
+                      beam_width=1000, mt_state625=random.getstate()[1], visited_log2=log2)
+
+
+def _keys(rng, n_heavy, heavy_pool, n_light, light_pool):
+    from splendor_amd.codec import state_key
+    root = np.uint64(state_key((), (0, 0, 0, 0, 0)) & (2**64 - 1))
+    pool_h = rng.integers(1, 2**63, size=heavy_pool, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    pool_l = rng.integers(1, 2**63, size=light_pool, dtype=np.uint64) * np.uint64(2)
+    k = np.concatenate([pool_h[rng.integers(0, heavy_pool, n_heavy)], pool_l[rng.integers(0, light_pool, n_light)]])
+    k = k[(k != root) & (k != np.uint64(2**64 - 1))]
+    return k[rng.permutation(len(k))]
+
+
+@pytest.mark.parametrize('order', [[0, 1, 2, 3], [3, 2, 1, 0], [2, 0, 3, 1]])
+def test_claims_first_occurrence_under_contention(order):
+    rng = np.random.default_rng(len(order) * 7 + order[0])
+    keys = _keys(rng, 1_500_000, 3000, 1_500_000, 1_200_000)
+    n = len(keys)
+    first = np.zeros(n, np.uint8)
+    _, idx = np.unique(keys, return_index=True)
+    first[idx] = 1
+    b = _backend(21)   # 2M slots for ~1.1M distinct keys: ~55% load, long probe chains
+    try:
+        dkeys = torch.from_numpy(keys.view(np.int64)).to(b.device)
+        ret = b.answer_buffer(n)
+        b.owner_begin(n)
+        bounds = np.linspace(0, n, len(order) + 1).astype(np.int64)
+        for c in order:   # chunks claimed out of index order: earlier records displace later holders
+            a, e = int(bounds[c]), int(bounds[c + 1])
+            b.owner_claim(dkeys[a:e], [0], [a], ret)   # answers at the global record index
+        b.owner_finish(ret)
+        torch.cuda.synchronize()
+        got = ret.cpu().numpy()
+    finally:
+        b.close()
+    bad = np.nonzero(got != first)[0]
+    assert len(bad) == 0, f'{len(bad)} records settled wrongly, first at {bad[:5]}'
