@@ -101,6 +101,17 @@ class Comm:
         outs = list(out.split([int(x) for x in recv_sizes]))
         return out, dist.all_to_all(outs, list(pieces), async_op=True)
 
+    def alltoall_into(self, pieces, outs):
+        """all_to_all of pieces[o] (views) to rank o, received straight into the views outs[o]."""
+        if self.cpu_coll:
+            send = torch.cat([p.cpu() for p in pieces])
+            r = torch.empty(sum(int(o.numel()) for o in outs), dtype=send.dtype)
+            dist.all_to_all_single(r, send, [int(o.numel()) for o in outs], [int(p.numel()) for p in pieces])
+            for o, x in zip(outs, r.split([int(o.numel()) for o in outs])):
+                o.copy_(x.to(o.device))
+            return
+        dist.all_to_all(list(outs), list(pieces))
+
     @staticmethod
     def wait(handle):
         if handle is not None:
@@ -323,22 +334,45 @@ class DistSolve:
         src_tot = from_src.sum(axis=1)
         src_base = np.concatenate([[0], np.cumsum(src_tot)])        # global index base per source
         src_chunk = np.concatenate([np.zeros((c.world, 1), np.int64), np.cumsum(from_src, axis=1)], axis=1)
+        # this rank's own records never enter the exchange: they are claimed straight from send_key
+        # (no RCCL self-copy beside the claims; at world 1 there is no collective at all)
+        recv_x = from_src.copy()
+        recv_x[me, :] = 0
         handles = []
         for j in range(C):
             pieces = [send_key[int(ostart[o] + ochunk[j, o]):int(ostart[o] + ochunk[j + 1, o])]
                       for o in range(c.world)]
-            handles.append(c.alltoall_pieces(pieces, from_src[:, j]))
+            self_piece = pieces[me]
+            if c.world > 1:
+                pieces[me] = send_key[:0]
+                rkey, hd = c.alltoall_pieces(pieces, recv_x[:, j])
+            else:
+                rkey, hd = send_key[:0], None
+            handles.append((self_piece, rkey, hd))
         n_own = int(src_tot.sum())
         b.owner_begin(n_own)
         ret = b.answer_buffer(n_own)
-        for j, (rkey, hd) in enumerate(handles):
+        for j, (self_piece, rkey, hd) in enumerate(handles):
+            if self_piece.numel():   # no wait: claims of any order settle to first occurrence
+                b.owner_claim(self_piece, [0], [int(src_base[me] + src_chunk[me, j])], ret)
             c.wait(hd)
-            starts = np.concatenate([[0], np.cumsum(from_src[:, j])[:-1]])
-            bases = src_base[:-1] + src_chunk[:, j]
-            b.owner_claim(rkey, starts, bases, ret)
+            if rkey.numel():
+                starts = np.concatenate([[0], np.cumsum(recv_x[:, j])[:-1]])
+                bases = src_base[:-1] + src_chunk[:, j]
+                b.owner_claim(rkey, starts, bases, ret)
         b.owner_finish(ret)
         self._mark(st, 'a2a_keys+claim')
-        back = c.alltoall(ret, src_tot, ostart[1:] - ostart[:-1])
+        # answers back to the sources; this rank's own answers are copied, not exchanged
+        own_sz = ostart[1:] - ostart[:-1]
+        mine_ret = ret[int(src_base[me]):int(src_base[me + 1])]
+        if c.world > 1:
+            back = b.answer_buffer(int(ostart[-1]))
+            pieces = [ret[int(src_base[q]):int(src_base[q + 1])] if q != me else ret[:0] for q in range(c.world)]
+            outs = [back[int(ostart[o]):int(ostart[o + 1])] if o != me else back[:0] for o in range(c.world)]
+            c.alltoall_into(pieces, outs)
+            back[int(ostart[me]):int(ostart[me + 1])].copy_(mine_ret)
+        else:
+            back = mine_ret
         n_loc = b.apply(back)
         self._mark(st, 'dedup_exchange')
         all_n = c.allgather_int(n_loc)
