@@ -105,9 +105,10 @@ class Comm:
         """all_to_all of pieces[o] (views) to rank o, received straight into the views outs[o]."""
         if self.cpu_coll:
             send = torch.cat([p.cpu() for p in pieces])
-            r = torch.empty(sum(int(o.numel()) for o in outs), dtype=send.dtype)
-            dist.all_to_all_single(r, send, [int(o.numel()) for o in outs], [int(p.numel()) for p in pieces])
-            for o, x in zip(outs, r.split([int(o.numel()) for o in outs])):
+            rows = [int(o.shape[0]) for o in outs]
+            r = torch.empty((sum(rows),) + tuple(outs[0].shape[1:]), dtype=send.dtype)
+            dist.all_to_all_single(r, send, rows, [int(p.shape[0]) for p in pieces])
+            for o, x in zip(outs, r.split(rows)):
                 o.copy_(x.to(o.device))
             return
         dist.all_to_all(list(outs), list(pieces))
@@ -408,8 +409,18 @@ class DistSolve:
         self._mark(st, 'select')
         rec = b.pack_kept()
         self._mark(st, 'pack_kept')
-        recv = c.alltoall_counts(dest_counts)
-        rrec = c.alltoall(rec, dest_counts, recv)
+        if c.world > 1:   # records arrive source rank by source rank; this rank's own are copied
+            recv = c.alltoall_counts(dest_counts)
+            me = c.rank
+            so = np.concatenate([[0], np.cumsum(dest_counts)]).astype(np.int64)
+            ro = np.concatenate([[0], np.cumsum(recv)]).astype(np.int64)
+            rrec = torch.empty((int(ro[-1]),) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
+            pieces = [rec[int(so[q]):int(so[q + 1])] if q != me else rec[:0] for q in range(c.world)]
+            outs = [rrec[int(ro[q]):int(ro[q + 1])] if q != me else rrec[:0] for q in range(c.world)]
+            c.alltoall_into(pieces, outs)
+            rrec[int(ro[me]):int(ro[me + 1])].copy_(rec[int(so[me]):int(so[me + 1])])
+        else:
+            rrec = rec
         self._mark(st, 'a2a_kept')
         b.receive(rrec, self.heur)
         self._turn_sync()
