@@ -165,6 +165,10 @@ int sbd_owner_begin(sb_engine* e, int64_t n_total);
 int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, int64_t n, int32_t nseg, const int64_t* seg_start,
                     const int64_t* seg_base, uint8_t* d_ret);
 int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
+/* answers over the wire as bits: dst[i] = bit k set iff src[8i + k] != 0 (n bytes -> ceil(n/8));
+ * unpack is the inverse (n answer bytes from ceil(n/8) packed bytes).  Both on the engine stream. */
+int sbd_pack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
+int sbd_unpack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
 /* apply the answers (in pack order); *n_unique_local = this rank's next_queue entries */
 int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
 /* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */

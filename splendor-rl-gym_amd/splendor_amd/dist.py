@@ -366,11 +366,21 @@ class DistSolve:
         # answers back to the sources; this rank's own answers are copied, not exchanged
         own_sz = ostart[1:] - ostart[:-1]
         mine_ret = ret[int(src_base[me]):int(src_base[me + 1])]
-        if c.world > 1:
+        if c.world > 1:   # one bit per answer on the wire (8x less than the answer bytes)
+            nb = lambda x: (int(x) + 7) // 8
+            sp = np.concatenate([[0], np.cumsum([nb(src_tot[q]) if q != me else 0 for q in range(c.world)])])
+            rp = np.concatenate([[0], np.cumsum([nb(own_sz[o]) if o != me else 0 for o in range(c.world)])])
+            sbits = b.answer_buffer(int(sp[-1]))
+            rbits = b.answer_buffer(int(rp[-1]))
+            for q in range(c.world):
+                if q != me:
+                    b.pack_bits(ret[int(src_base[q]):int(src_base[q + 1])], sbits[int(sp[q]):int(sp[q + 1])])
+            c.alltoall_into([sbits[int(sp[q]):int(sp[q + 1])] for q in range(c.world)],
+                            [rbits[int(rp[o]):int(rp[o + 1])] for o in range(c.world)])
             back = b.answer_buffer(int(ostart[-1]))
-            pieces = [ret[int(src_base[q]):int(src_base[q + 1])] if q != me else ret[:0] for q in range(c.world)]
-            outs = [back[int(ostart[o]):int(ostart[o + 1])] if o != me else back[:0] for o in range(c.world)]
-            c.alltoall_into(pieces, outs)
+            for o in range(c.world):
+                if o != me:
+                    b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o + 1])])
             back[int(ostart[me]):int(ostart[me + 1])].copy_(mine_ret)
         else:
             back = mine_ret
@@ -520,6 +530,8 @@ class HipBackend:
         lib.sbd_owner_begin.argtypes = [vp, i64]
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_owner_finish.argtypes = [vp, vp]
+        lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
+        lib.sbd_unpack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_apply.argtypes = [vp, vp, p64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_key_range.argtypes = [vp, vp]
@@ -612,6 +624,15 @@ class HipBackend:
 
     def owner_finish(self, ret):
         self._chk(self.lib.sbd_owner_finish(self.h, ret.data_ptr()), 'sbd_owner_finish')
+
+    def pack_bits(self, src, dst):
+        """dst (ceil(n/8) bytes) <- the n answer bytes of src as bits (bit k of byte i = src[8i + k])."""
+        if src.numel():
+            self._chk(self.lib.sbd_pack_bits(self.h, src.data_ptr(), src.numel(), dst.data_ptr()), 'sbd_pack_bits')
+
+    def unpack_bits(self, src, dst):
+        if dst.numel():
+            self._chk(self.lib.sbd_unpack_bits(self.h, src.data_ptr(), dst.numel(), dst.data_ptr()), 'sbd_unpack_bits')
 
     def apply(self, back):
         n = self.C.c_int64()

@@ -58,3 +58,26 @@ def test_claims_first_occurrence_under_contention(order):
         b.close()
     bad = np.nonzero(got != first)[0]
     assert len(bad) == 0, f'{len(bad)} records settled wrongly, first at {bad[:5]}'
+
+
+def test_answer_bits_roundtrip():
+    """sbd_pack_bits / sbd_unpack_bits (answers on the wire as bits) at unaligned offsets and lengths."""
+    rng = np.random.default_rng(5)
+    b = _backend(12)
+    try:
+        for n, off in ((0, 0), (1, 3), (7, 1), (8, 0), (9, 5), (1000, 13), (123457, 7)):
+            src = (rng.random(n + off + 3) < 0.4).astype(np.uint8) * rng.integers(1, 255, n + off + 3).astype(np.uint8)
+            ds = torch.from_numpy(src).to(b.device)
+            packed = torch.zeros((n + 7) // 8 + 2, dtype=torch.uint8, device=b.device)
+            b.pack_bits(ds[off:off + n], packed[1:1 + (n + 7) // 8])
+            out = torch.full((n + off + 3,), 7, dtype=torch.uint8, device=b.device)
+            b.unpack_bits(packed[1:1 + (n + 7) // 8], out[off:off + n])
+            torch.cuda.synchronize()
+            p = packed.cpu().numpy()
+            want = np.packbits((src[off:off + n] != 0).astype(np.uint8), bitorder='little')
+            assert np.array_equal(p[1:1 + len(want)], want) and p[0] == 0 and p[-1] == 0, n
+            o = out.cpu().numpy()
+            assert np.array_equal(o[off:off + n], (src[off:off + n] != 0).astype(np.uint8)), n
+            assert (o[:off] == 7).all() and (o[off + n:] == 7).all(), n
+    finally:
+        b.close()
