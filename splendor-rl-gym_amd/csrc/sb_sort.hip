@@ -387,13 +387,21 @@ __device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((s
 
 // histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
 // cluster); 16 loads in flight per thread
+#ifndef SB_OSH_GRID
+#define SB_OSH_GRID 1024     // 4 blocks per CU: LDS atomic latency hidden (256: 1 per CU, 2x slower)
+#endif
+#ifndef SB_OSH_WH
+#define SB_OSH_WH 1          // per-wave sub-histograms (less LDS atomic contention between waves)
+#endif
+constexpr int OSH_NH = SB_OSH_WH ? OS_NW : 1;
 __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
                                                    const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
-    __shared__ uint32_t h[8][256];
+    __shared__ uint32_t hh[OSH_NH][8][256];
     const int P = sort_passes(st);
     const uint64_t slo = st[ST_SLO];
-    for (int i = threadIdx.x; i < 8 * 256; i += OS_NT) (&h[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < OSH_NH * 8 * 256; i += OS_NT) (&hh[0][0][0])[i] = 0;
     __syncthreads();
+    uint32_t (*h)[256] = hh[SB_OSH_WH ? (threadIdx.x >> 6) : 0];
     const uint64_t lt = lanemask_lt();
     const int64_t stride = (int64_t)gridDim.x * OS_NT;
     for (int64_t i0 = (int64_t)blockIdx.x * OS_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
@@ -420,7 +428,9 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
     __syncthreads();
     uint32_t* gh = reinterpret_cast<uint32_t*>(lb);
     for (int i = threadIdx.x; i < P * 256; i += OS_NT) {
-        const uint32_t c = (&h[0][0])[i];
+        uint32_t c = 0;
+#pragma unroll
+        for (int v = 0; v < OSH_NH; v++) c += (&hh[v][0][0])[i];
         if (c) atomicAdd(&gh[i], c);
     }
 }
@@ -659,7 +669,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
     s.os.ensure(lb_words);
     SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
-    hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, 256)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
+    hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
     for (int p = 0; p < 8; p++)
         hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntiles), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p);
