@@ -363,7 +363,10 @@ __global__ void k_tk_sortsetup(uint64_t* st, int selected) {
 // flag, so no fence is needed.  The granules are zeroed once per sort call (memset); a predecessor
 // always holds an earlier ticket, so it is resident and the wait ends.
 constexpr int OS_NT = 256;
-constexpr int OS_IPT = 16;
+#ifndef SB_OS_IPT
+#define SB_OS_IPT 16
+#endif
+constexpr int OS_IPT = SB_OS_IPT;
 constexpr int OS_TILE = OS_NT * OS_IPT;   // 4096
 constexpr int OS_NW = OS_NT / 64;
 constexpr uint64_t OS_AGG = 1ull << 32, OS_INC = 2ull << 32;
