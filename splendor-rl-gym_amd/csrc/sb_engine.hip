@@ -915,7 +915,10 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         unsigned long long* krange = topk_range_reset(E.topk, E.s, fused, (E.cfg.flags & 8) != 0);
         unsigned long long* fh = topk_fused_hist(E.topk);
         const uint64_t* fb = topk_fused_base(E.topk);
-        const unsigned egf = grid_cap(n, 256, 2048);   // fewer blocks: one histogram flush per block
+#ifndef SB_EMIT_GRID
+#define SB_EMIT_GRID 1536   // = resident blocks (24 KB LDS: 6 per CU): no partial second round of blocks
+#endif
+        const unsigned egf = grid_cap(n, 256, SB_EMIT_GRID);   // fewer blocks: one histogram flush per block
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
     hipLaunchKernelGGL((k_emit_w<H, false>), dim3(egf), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, \
