@@ -6,11 +6,12 @@ from splendor_amd.engine import HEURISTIC_IDS, BeamEngine
 random.seed(0)
 st = random.getstate()[1]
 eng = BeamEngine(goal_pts=255, use_heuristic=True, heuristic=1, beam_width=4_000_000, mt_state625=st, device=0, timing=True)
-for i in range(16):
+NSTEPS = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+for i in range(NSTEPS):
     t0 = time.perf_counter()
     r = eng.step()
     dt = time.perf_counter() - t0
     print(i, eng.turn, r['n_parents'], r['n_unique'], f"host_ms={dt*1e3:.2f} noise_wait={r['ms_sort']:.2f} draws={r['noise_draws']}", flush=True)
 eng.sync()
-for t in range(1, 15):
+for t in range(max(1, NSTEPS - 60), NSTEPS - 1):
     print(t, {k: round(v, 3) for k, v in eng.turn_times(t).items()})
