@@ -198,7 +198,8 @@ int sbd_noise_fill(sb_engine* e, int32_t m, const void* wins, const uint64_t* ac
  * (kmin ^ 2^63, ~(kmax ^ 2^63)); sbd_sel_begin = select state for npos (<= 15) positions (1-based ranks
  * in score-descending order) below the bits common to the reduced range; per pass: sbd_sel_hist
  * (npos x 1024 int64 histogram of the next 10-bit digit per distinct prefix into hist_dev, over the keys
- * (src 0) or the candidates (src 1)), an all_reduce(SUM) of hist_dev by the caller on the same stream,
+ * (src 0) or the candidates (src 1); hist_dev must be zero on entry: fresh, or as the previous
+ * sbd_sel_pick left it), an all_reduce(SUM) of hist_dev by the caller on the same stream,
  * sbd_sel_pick; passes after the last digit are no-ops, so the caller runs a fixed 7 (ceil(64/10)).
  * After the first pass sbd_sel_compact keeps the keys of the chosen buckets as candidates.
  * sbd_sel_eq: count of keys equal to position 0's key (int64 at eq_dev) for the all_gather of the
@@ -206,7 +207,7 @@ int sbd_noise_fill(sb_engine* e, int32_t m, const void* wins, const uint64_t* ac
 int sbd_key_range(sb_engine* e, void* range_dev);
 int sbd_sel_begin(sb_engine* e, int32_t npos, const int64_t* positions, const void* range_dev);
 int sbd_sel_hist(sb_engine* e, int32_t src, void* hist_dev);
-int sbd_sel_pick(sb_engine* e, const void* hist_dev);
+int sbd_sel_pick(sb_engine* e, void* hist_dev);   /* also clears hist_dev for the next pass */
 int sbd_sel_compact(sb_engine* e);
 int sbd_sel_eq(sb_engine* e, void* eq_dev);
 /* kept = key > T or (key == T and global tie index < its position) [if has_top; T = position 0's key,

@@ -77,7 +77,7 @@ class Comm:
 
     def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
         send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
-        recv = torch.zeros_like(send)
+        recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send)
         return recv.cpu().numpy()
 
