@@ -224,10 +224,11 @@ def main():
         'cpu_baseline': None,
     }
     if dom == 'ms_expand':
-        # the bound that actually binds k_expand: random 128-B line touches — one probe
-        # load per raw child, a CAS + atomicMin per new key (= per survivor), lost marks not counted
-        # (a lower bound) — against the measured random 16-B load rate over a 32 GiB table
-        touches = (raw + 2 * uniq) / len(per)
+        # the bound that actually binds k_expand: random 128-B line requests — one probe
+        # load per raw child and one tag CAS per new key (= per survivor; its key store follows on the
+        # same line), lost marks not counted (a lower bound) — against the measured random 16-B load
+        # rate over a 32 GiB table
+        touches = (raw + uniq) / len(per)
         out['roofline']['random_access'] = {
             'touches_per_launch': int(touches), 'achieved_G_per_s': round(touches / (ms_dom * 1e-3) / 1e9, 2),
             'peak_G_per_s': RANDOM_LOAD_PEAK_G, 'frac': round(touches / (ms_dom * 1e-3) / 1e9 / RANDOM_LOAD_PEAK_G, 3),
