@@ -143,6 +143,11 @@ __device__ __forceinline__ bool claim_lm(Entry* __restrict__ tab, uint64_t mask,
     if (r == 1) atomicAdd(err + 2, 1u);
     else if (r == 0 && cur < (tag & ~((1ull << 40) - 1))) atomicAdd(err + 1, 1u);
     else if (r == 0 && cur < tag) atomicAdd(err + 3, 1u);
+    // err[6]: the key is already held by a same-turn child of the same 32-parent k_expand group
+    // (the share an in-LDS pre-dedup of a group's children would take off the visited set)
+    if (r == 0 && cur != EMPTY && cur >= (tag & ~((1ull << 40) - 1)) &&
+        (((cur >> 8) & 0xFFFFFFFFull) >> 5) == (((tag >> 8) & 0xFFFFFFFFull) >> 5))
+        atomicAdd(err + 6, 1u);
 #endif
     if (r != 0) return r == 1;
     if (cur < tag) return false;
@@ -871,8 +876,9 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     }
     check_err_word(E);
 #ifdef SB_CLAIM_STATS
-    fprintf(stderr, "claims turn %d: old %u inserted %u early-out %u lost-at-min %u displaced %u\n", E.turn,
-            E.h_small[3], E.h_small[4], E.h_small[5], E.h_small[6], E.h_small[7]);
+    // err = d_small + 1: err[k] is h_small[k + 1]
+    fprintf(stderr, "claims turn %d: old %u inserted %u early-out %u lost-at-min %u displaced %u in-group-dup %u\n",
+            E.turn, E.h_small[2], E.h_small[3], E.h_small[4], E.h_small[5], E.h_small[6], E.h_small[7]);
 #endif
     const bool heur = E.cfg.use_heuristic != 0;
     const int64_t nu = E.h_small[0];
