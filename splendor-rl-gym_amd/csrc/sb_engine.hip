@@ -200,8 +200,8 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
 #define SB_XP_PAR 32
 #endif
 #ifndef SB_XP_WAVES
-#define SB_XP_WAVES 1
-#endif
+#define SB_XP_WAVES 8   // min waves per SIMD: caps VGPRs at 64 (a 24 B/lane spill) for 8 waves; with
+#endif                  // 16-bit queues (17 KB LDS) the block fits 9 per CU: more probes in flight
 #ifndef SB_XP_NT
 #define SB_XP_NT 256
 #endif
@@ -215,6 +215,7 @@ constexpr int XP_U = SB_XP_U;
 #endif
 constexpr int XP_NT = SB_XP_NT;       // 4 waves
 constexpr int XP_PAR = SB_XP_PAR;     // parents per block iteration (<= 32)
+static_assert(XP_PAR <= 32 && (31 | ((NCARDS + 127) << 5)) <= 0xFFFF, "k_expand queue entries: 5-bit s, 16-bit entry");
 
 struct XpShared {
     uint32_t card[NCARDS];
@@ -230,8 +231,10 @@ struct XpShared {
     uint32_t pbon[XP_PAR];
     int32_t pbk[XP_PAR];
     unsigned long long cmask[XP_PAR][3];
-    uint32_t qb[XP_PAR * NCARDS];     // buy children (s | dsc << 5)
-    uint32_t qt[XP_PAR * NPAT_MAX];   // take children: phase B runs all buys, then all takes, so a
+    // 16-bit entries (s < 32, dsc < 192: 13 bits): the queues are most of the block's LDS, and LDS is
+    // what bounds k_expand's occupancy (29.5 KB/block with 32-bit entries: 5 blocks per CU)
+    uint16_t qb[XP_PAR * NCARDS];     // buy children (s | dsc << 5)
+    uint16_t qt[XP_PAR * NPAT_MAX];   // take children: phase B runs all buys, then all takes, so a
     uint32_t nqb, nqt, nraw;          // wave rarely mixes the two (a buy re-hashes its card tuple)
     uint32_t grp[3];                  // this, next and next-but-one parent group
 };
@@ -360,11 +363,11 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             }
             qb = __shfl(qb, 0, 64);
             qt = __shfl(qt, 0, 64);
-            if ((bl >> lane) & 1) S.qb[qb + __popcll(bl & lt)] = (uint32_t)s | ((uint32_t)lane << 5);
+            if ((bl >> lane) & 1) S.qb[qb + __popcll(bl & lt)] = (uint16_t)(s | (lane << 5));
             if (lane < 26 && ((bh >> lane) & 1))
-                S.qb[qb + nbl + __popc(bh & (uint32_t)lt)] = (uint32_t)s | ((uint32_t)(64 + lane) << 5);
-            if ((t0 >> lane) & 1) S.qt[qt + __popcll(t0 & lt)] = (uint32_t)s | ((uint32_t)(NCARDS + lane) << 5);
-            if ((t1 >> lane) & 1) S.qt[qt + nt0 + __popcll(t1 & lt)] = (uint32_t)s | ((uint32_t)(NCARDS + 64 + lane) << 5);
+                S.qb[qb + nbl + __popc(bh & (uint32_t)lt)] = (uint16_t)(s | ((64 + lane) << 5));
+            if ((t0 >> lane) & 1) S.qt[qt + __popcll(t0 & lt)] = (uint16_t)(s | ((NCARDS + lane) << 5));
+            if ((t1 >> lane) & 1) S.qt[qt + nt0 + __popcll(t1 & lt)] = (uint16_t)(s | ((NCARDS + 64 + lane) << 5));
         }
         __syncthreads();
         // ---- phase B: dense child processing: key, visited probe + claim; XP_U children per thread
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
 #pragma unroll
             for (int u = 0; u < XP_U; u++) {
                 const uint32_t i = i0 + u * XP_NT;
-                e[u] = i < nqb ? S.qb[i] : (i < nq ? S.qt[i - nqb] : 0xFFFFFFFFu);
+                e[u] = i < nqb ? (uint32_t)S.qb[i] : (i < nq ? (uint32_t)S.qt[i - nqb] : 0xFFFFFFFFu);
                 key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
             }
 #pragma unroll
