@@ -35,8 +35,9 @@ def main():
                 env = dict(os.environ, SPLENDOR_BEAM_LIB=os.path.join(VDIR, f))
                 if mode == 'sharded':
                     env['SB_FORCE_DIST'] = '1'
+                extra = ['--realistic'] if '--realistic' in sys.argv else []   # config C4 instead of C3
                 r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--no-cpu-baseline', '--steps',
-                                    steps], env=env, capture_output=True, text=True, timeout=300)
+                                    steps] + extra, env=env, capture_output=True, text=True, timeout=300)
                 line = [l for l in r.stdout.splitlines() if l.startswith('{')]
                 if not line:
                     print(f, mode, 'FAILED', r.stderr[-500:], flush=True)
