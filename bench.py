@@ -3,12 +3,20 @@
 
 Workload (N=1): config C3 of BASELINE.json — speedrun goal 15, -u -H balanced, beam_width 4,000,000,
 random.seed(0) (the largest single-GPU config; C2 at W=300k is a parity case, not a bench line).
-The engine runs the seeded solve from the root; the steps until the beam first fills (turns 0..8)
-are setup, then `--warmup` untimed steps, then exactly `--steps` timed steps.  A step is one full
-sb_step: goal check, expansion + hash + visited claim, survivor check, next_queue scan, state/score
-emission with MT19937 noise, stable top-k, beam write.  The goal is raised to 255 for the timing run
-so that more than the 6 saturated turns of the goal-15 trajectory can be timed; up to turn 15 the
-trajectory is identical to the goal-15 solve (the goal is first reached at turn 15).
+
+Only C3's own saturated steps are timed.  A probe solve (untimed, also the warmup) finds the window:
+the steps whose queue is full (n_parents == W) and holds no goal state, i.e. turns 9..14 of the seeded
+goal-15 trajectory (the goal check of turn 15 ends the solve, src/solver.py:438-445).  `--steps K`
+beyond one window replays it: a fresh engine with the same seed is set up outside the timed region
+(turns 0..8) and its window is timed again.  Every timed segment is bracketed by a device sync (and a
+barrier with N > 1); `ms_per_step` = the summed segment time / K.  A step is one full sb_step: goal
+check, expansion + hash + visited claim, survivor count, next_queue scan, state/score emission with
+MT19937 noise, stable top-k, beam write (the expansion of the next queue is pipelined behind the gather,
+so a timed window of turns t..u covers the expansions of queues t+1..u+1).
+
+--gpus N > 1: one process per GPU over RCCL (bench_dist.py, the sharded step).  Without a launcher
+environment the script starts `torch.distributed.run` itself (before any GPU call) and exits with its
+return code.
 
 Output: one JSON line (rank 0) with `roofline` for the dominant kernel (device events on the engine's
 stream) and `cpu_baseline` (the C oracle, single thread, same config and seed, bounded sample).
@@ -17,6 +25,8 @@ import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,18 +37,28 @@ sys.path.insert(0, os.path.join(REPO, 'oracle'))
 METRIC = 'states expanded/sec per beam step, goal=15 beam_width=4M, 1/2/4/8 MI355X'
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 RANDOM_LOAD_PEAK_G = 48.0   # random 16-B loads / s over a 32 GiB table, measured (profiles/micro/r1_randaccess.txt)
+GOAL = 15                   # C3 / C5 goal_pts
+# the reference's own CPU path on C3's heuristic, measured in the build container (BASELINE.md §2 / SURVEY §6):
+# pure Python, 1 core; it cannot run on the GPU box (the reference does not travel), so it is quoted, not timed
+PY_REFERENCE = {'balanced': (11421, 'goal 15 -u -H balanced W=1M, saturated step 87.6 s'),
+                'efficiency': (8323, 'goal 15 -u -H efficiency W=300k, saturated step 36.0 s (3 runs sharing 8 cores)'),
+                'simple': (13093, 'goal 15 -u -H simple W=300k, saturated step 22.9 s')}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--width', type=int, default=4_000_000)
-    ap.add_argument('--heuristic', default='balanced')
+    ap.add_argument('--steps', type=int, default=12)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--width', type=int, default=4_000_000, help='beam width per GPU')
+    ap.add_argument('--heuristic', default=None,
+                    help='default: balanced (C3) on one GPU, efficiency (C5) on the sharded path')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget-s', type=float, default=30.0)
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launcher plumbing only (CPU, gloo): every rank joins the group, rank 0 prints the world; '
+                         'no GPU call (tests/test_bench_launch.py)')
     ap.add_argument('--realistic', action='store_true',
                     help='config C4 instead: realistic 2-player goal 15 --shuffle, W=1M (a separate line, not the '
                          'headline metric)')
@@ -98,92 +118,196 @@ def cpu_baseline(width, heuristic, seed, budget_s):
     if best is None:
         return None
     t, n, dt = best
-    return {'value': round(n / dt, 1), 'unit': 'states/s', 'cores': 1, 'kind': 'port',
-            'sample': f'C oracle (oracle/csrc/oracle.c), 1 thread, same config and seed; turn {t} '
-                      f'({n} parents) of the W={width} trajectory, {dt:.2f} s; host cores '
-                      f'available {len(os.sched_getaffinity(0))}'}
+    out = {'value': round(n / dt, 1), 'unit': 'states/s', 'cores': 1, 'kind': 'port',
+           'sample': f'C oracle (oracle/csrc/oracle.c), 1 thread, same config and seed; turn {t} '
+                     f'({n} parents) of the W={width} trajectory, {dt:.2f} s; host cores '
+                     f'available {len(os.sched_getaffinity(0))}'}
+    if heuristic in PY_REFERENCE:
+        v, what = PY_REFERENCE[heuristic]
+        out['python_reference'] = {
+            'value': v, 'unit': 'states/s', 'cores': 1,
+            'source': f'the reference itself (src/solver.py, CPython 3.10) on {what}, measured in the build '
+                      'container (BASELINE.md §2); quoted, not timed here: the reference cannot travel to the GPU box'}
+    return out
+
+
+class Window:
+    """Feeds the timed loop with C3-window steps: each engine is set up (untimed) from the root with the
+    same seed up to the first saturated turn; `left` steps of its window remain.  `make()` builds a
+    seeded engine; `step(e)` / `sync(e)` / `close(e)` drive it."""
+
+    def __init__(self, make, step, sync, close, first, length):
+        self.make, self._step, self._sync, self._close = make, step, sync, close
+        self.first, self.length = first, length   # window turns first .. first+length-1
+        self.eng, self.left, self.engines = None, 0, 0
+
+    def ensure(self):
+        if self.left > 0:
+            return
+        if self.eng is not None:
+            self._close(self.eng)
+            self.eng = None
+        self.eng = self.make()
+        self.engines += 1
+        for _ in range(self.first):   # setup: turns 0 .. first-1
+            r = self._step(self.eng)
+            assert not r['done'], 'setup reached the goal'
+        self.left = self.length
+        self._sync(self.eng)
+
+    def step(self):
+        self.left -= 1
+        r = self._step(self.eng)
+        assert not r['done'], 'stepped past the window'
+        return r
+
+    def close(self):
+        if self.eng is not None:
+            self._close(self.eng)
+            self.eng = None
+
+
+def probe_window(make, step, close, width):
+    """Run one seeded solve to its goal: (first saturated turn, window length, turns, moves).  The window
+    is the steps whose queue is full and has no goal state (every later step of the solve ends it)."""
+    eng = make()
+    turn, first, last = 0, None, None
+    while True:
+        r = step(eng)
+        if r['done']:
+            break
+        if r['n_parents'] >= width and first is None:
+            first = turn
+        if first is not None:
+            last = turn
+        turn += 1
+    close(eng)
+    if first is None:
+        raise RuntimeError('the beam never saturates before the goal: nothing to time')
+    return first, last - first + 1, turn
+
+
+def timed_steps(win, steps, warmup, sync_all, on_segment=None):
+    """Warmup then exactly `steps` timed window steps, segment by segment (a segment ends where an
+    engine's window ends); returns (per-step stats, total seconds)."""
+    for _ in range(warmup):
+        win.ensure()
+        win.step()
+    per, total = [], 0.0
+    while len(per) < steps:
+        win.ensure()
+        n = min(steps - len(per), win.left)
+        turn0 = win.first + win.length - win.left
+        sync_all(win.eng)
+        t0 = time.perf_counter()
+        seg = [win.step() for _ in range(n)]
+        sync_all(win.eng)
+        total += time.perf_counter() - t0
+        if on_segment:
+            on_segment(win.eng, turn0, seg)
+        per += seg
+    return per, total
 
 
 def run_single(args):
     from splendor_amd.engine import HEURISTIC_IDS, BeamEngine
-    random.seed(args.seed)
-    st = random.getstate()[1]
-    eng = BeamEngine(goal_pts=255, use_heuristic=True, heuristic=HEURISTIC_IDS[args.heuristic],
-                     beam_width=args.width, mt_state625=st, device=0, timing=True)
-    setup_turns = 0
-    while True:   # setup: until the beam is full
-        r = eng.step()
-        setup_turns += 1
-        if r['n_kept'] >= args.width or r['done']:
-            break
-    for _ in range(args.warmup):
-        eng.step()
-    eng.sync()
-    per = []
-    turn0 = eng.turn
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        per.append(eng.step())
-    eng.sync()
-    elapsed = time.perf_counter() - t0
-    # device phase times of the timed turns (HIP events recorded on the engine's stream)
-    for i, p in enumerate(per):
-        p.update(eng.turn_times(turn0 + i))
-    eng.close()
-    return per, elapsed, setup_turns
+    heur = args.heuristic
+
+    def make():
+        random.seed(args.seed)
+        return BeamEngine(goal_pts=GOAL, use_heuristic=True, heuristic=HEURISTIC_IDS[heur],
+                          beam_width=args.width, mt_state625=random.getstate()[1], device=0, timing=True)
+
+    first, length, turns = probe_window(make, lambda e: e.step(), lambda e: e.close(), args.width)
+    win = Window(make, lambda e: e.step(), lambda e: e.sync(), lambda e: e.close(), first, length)
+
+    def phases(eng, turn0, seg):   # device phase times (HIP events recorded on the engine's stream)
+        for i, p in enumerate(seg):
+            p.update(eng.turn_times(turn0 + i))
+
+    per, elapsed = timed_steps(win, args.steps, args.warmup, lambda e: e.sync(), phases)
+    win.close()
+    return per, elapsed, (first, length, turns, win.engines)
 
 
 def run_realistic(args):
     """Config C4: MultiPlayerState beam search, 2 players, goal 15, shuffled market (seed 0), W=1M."""
+    from splendor_amd import _lib
     from splendor_amd.engine_rt import RealisticEngine
     from splendor_amd.realistic import GameConfig, MultiPlayerState
     width = args.width if args.width != 4_000_000 else 1_000_000
     cfg = GameConfig(num_players=2, target_points=15, gems_per_color=4, infinite_resources=False)
-    root = MultiPlayerState.newgame(config=cfg, shuffle_market=True, seed=args.seed)
-    random.seed(args.seed)
-    eng = RealisticEngine(root, beam_width=width, mt_state625=random.getstate()[1], device=0)
-    setup = 0
-    while True:
-        r = eng.step()
-        setup += 1
-        if r['n_kept'] >= width or r['done']:
-            break
-    for _ in range(args.warmup):
-        eng.step()
-    import ctypes
-    from splendor_amd import _lib
-    _lib.lib().sb_sync(eng._h)
-    per = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        per.append(eng.step())
-        if per[-1]['done']:
-            break
-    _lib.lib().sb_sync(eng._h)
-    elapsed = time.perf_counter() - t0
-    eng.close()
+
+    def make():
+        root = MultiPlayerState.newgame(config=cfg, shuffle_market=True, seed=args.seed)
+        random.seed(args.seed)
+        return RealisticEngine(root, beam_width=width, mt_state625=random.getstate()[1], device=0)
+
+    sync = lambda e: _lib.lib().sb_sync(e._h)
+    first, length, turns = probe_window(make, lambda e: e.step(), lambda e: e.close(), width)
+    win = Window(make, lambda e: e.step(), sync, lambda e: e.close(), first, length)
+    per, elapsed = timed_steps(win, args.steps, args.warmup, sync)
+    win.close()
     parents = sum(p['n_parents'] for p in per)
     out = {'metric': 'states expanded/sec per beam step, realistic 2-player goal 15 --shuffle, beam_width=1M',
            'value': round(parents / elapsed, 1), 'unit': 'states/s', 'n_gpus': 1, 'steps': len(per),
            'warmup': args.warmup, 'ms_per_step': round(elapsed / len(per) * 1e3, 3), 'higher_is_better': True,
            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64+f64',
            'data': f'synthetic: seeded realistic solve trajectory (market shuffle seed {args.seed}, random.seed('
-                   f'{args.seed})), saturated turns {setup + args.warmup}..{setup + args.warmup + len(per) - 1}',
+                   f'{args.seed})); timed: saturated turns {first}..{first + length - 1} of the {turns}-move game, '
+                   f'replayed on {win.engines} seeded engines',
            'config': {'workload': f'realistic 2p goal_pts=15 --shuffle beam_width={width} (C4)', 'beam_width': width,
                       'b_raw': round(sum(p['n_raw'] for p in per) / parents, 3),
                       'b_uniq': round(sum(p['n_unique'] for p in per) / parents, 3)}}
     print(json.dumps(out))
 
 
+def self_launch(args):
+    """--gpus N > 1 without a launcher: one process per GPU via torch.distributed.run (child process; the
+    parent has not touched the GPU), exit with its code."""
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, SB_BENCH_LAUNCHED='1')
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    import torch.distributed as dist
+    if 'RANK' not in os.environ:
+        os.environ.update(RANK='0', LOCAL_RANK='0', WORLD_SIZE='1', MASTER_ADDR='127.0.0.1', MASTER_PORT='29542')
+    dist.init_process_group('gloo')
+    world = dist.get_world_size()
+    if world != args.gpus:
+        raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
+    dist.barrier()
+    if dist.get_rank() == 0:
+        print(json.dumps({'metric': METRIC, 'n_gpus': world, 'dry_run': True,
+                          'launched_by_bench': os.environ.get('SB_BENCH_LAUNCHED') == '1'}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    launched = 'RANK' in os.environ or 'LOCAL_RANK' in os.environ
+    if args.gpus > 1 and not launched:
+        sys.exit(self_launch(args))
+    if args.dry_run:
+        return dry_run(args)
     if args.realistic:
         return run_realistic(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1 or args.gpus > 1 or os.environ.get('SB_FORCE_DIST') == '1':   # (diagnostic: sharded path at N=1)
+        if args.heuristic is None:
+            args.heuristic = 'efficiency'   # C5
         import bench_dist
         return bench_dist.main(args)
-    per, elapsed, setup_turns = run_single(args)
+    if args.heuristic is None:
+        args.heuristic = 'balanced'         # C3
+    per, elapsed, (first, length, turns, engines) = run_single(args)
     parents = sum(p['n_parents'] for p in per)
     raw = sum(p['n_raw'] for p in per)
     uniq = sum(p['n_unique'] for p in per)
@@ -211,11 +335,13 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'u64+f64',
-        'data': f'synthetic: seeded solve trajectory (random.seed({args.seed})), saturated turns '
-                f'{setup_turns + args.warmup}..{setup_turns + args.warmup + args.steps - 1}',
-        'config': {'workload': f'speedrun goal_pts=15 -u -H {args.heuristic} beam_width={args.width} (C3)',
+        'data': f'synthetic: seeded solve trajectory (random.seed({args.seed})); timed: the saturated turns '
+                f'{first}..{first + length - 1} of the {turns}-move goal-{GOAL} solve (queue full, no goal state), '
+                f'replayed on {engines} seeded engines set up outside the timed region',
+        'config': {'workload': f'speedrun goal_pts={GOAL} -u -H {args.heuristic} beam_width={args.width} (C3)',
                    'beam_width': args.width, 'heuristic': args.heuristic, 'seed': args.seed,
-                   'parallelism': 'single GPU', 'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3)},
+                   'parallelism': 'single GPU', 'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
+                   'timed_turns': [first, first + length - 1], 'moves': turns},
         'phases_ms': phases,
         'roofline': {'bound': 'hbm', 'kernel': dom.replace('ms_', 'k_'), 'achieved': round(achieved, 2),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),

@@ -1,14 +1,17 @@
 """bench.py --gpus N (N > 1): the sharded beam step, one process per GPU, RCCL over xGMI.
 
-Launched by `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...`.  Weak scaling:
-every GPU holds --width states (global beam_width = N x width; N=8 x 4M = 32M is config C5's width).
-The seeded solve runs from the root until the global beam is full (setup), then --warmup untimed
-steps, then exactly --steps timed steps, each bracketed by barrier + device synchronize; the time is
-the max over ranks and value = all parents expanded / that time.
+Launched by `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...` (bench.py starts
+that launcher itself when run without one).  Weak scaling: every GPU holds --width states (global
+beam_width = N x width; N=8 x 4M = 32M is config C5's width, heuristic `efficiency` by default).
+As on one GPU, only the solve's saturated window is timed (queue full, no goal state: a probe solve
+finds it, untimed), replayed on fresh seeded solves set up outside the timed region; each timed
+segment is bracketed by barrier + device synchronize, the time is the max over ranks and
+value = all parents expanded / that time.
 """
 import json
 import os
 import random
+import sys
 import time
 
 import numpy as np
@@ -17,12 +20,11 @@ import torch.distributed as dist
 
 
 def main(args):
-    import sys
     # RCCL prints its version banner on stdout at init: keep stdout for the one JSON line
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    from bench import HBM_PEAK_GBS, METRIC, step_bytes
+    from bench import GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, probe_window, step_bytes, timed_steps
     from splendor_amd.dist import Comm, DistSolve, HipBackend
     from splendor_amd.engine import HEURISTIC_IDS
     if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
@@ -35,28 +37,28 @@ def main(args):
     torch.cuda.set_device(dev)
     dist.init_process_group(backend, device_id=torch.device('cuda', dev) if backend == 'nccl' else None)
     rank, world = dist.get_rank(), dist.get_world_size()
+    if world != args.gpus and not (args.gpus == 1 and os.environ.get('SB_FORCE_DIST') == '1'):
+        raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
     W = args.width * world
-    random.seed(args.seed)
-    st = random.getstate()[1]
-    b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=255, use_heuristic=True,
-                   heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=st)
-    comm = Comm(b.device)
-    solve = DistSolve(b, comm, goal_pts=255, use_heuristic=True, beam_width=W)
-    setup = 0
-    while True:
-        s = solve.step()
-        setup += 1
-        if s.get('n_kept', 0) >= W or s['done']:
-            break
-    for _ in range(args.warmup):
-        solve.step()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    per = [solve.step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = time.perf_counter() - t0
+
+    def make():
+        random.seed(args.seed)
+        b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=GOAL, use_heuristic=True,
+                       heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1])
+        return DistSolve(b, Comm(b.device), goal_pts=GOAL, use_heuristic=True, beam_width=W)
+
+    def close(s):
+        s.b.close()
+
+    def sync_all(_s):
+        torch.cuda.synchronize()
+        dist.barrier()
+
+    first, length, turns = probe_window(make, lambda s: s.step(), close, W)
+    win = Window(make, lambda s: s.step(), lambda s: torch.cuda.synchronize(), close, first, length)
+    per, el = timed_steps(win, args.steps, args.warmup, sync_all)
+    win.close()
+    comm = Comm(torch.device('cuda', dev))
     el_max = float(comm.allreduce(np.array([int(el * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9
     parents = sum(p['n_parents'] for p in per)
     raw = sum(p['n_raw'] for p in per)
@@ -71,20 +73,24 @@ def main(args):
             'metric': METRIC, 'value': round(parents / el_max, 1), 'unit': 'states/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el_max / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64+f64',
-            'data': f'synthetic: seeded solve trajectory (random.seed({args.seed})), saturated turns '
-                    f'{setup + args.warmup}..{setup + args.warmup + args.steps - 1}',
-            'config': {'workload': f'speedrun goal_pts=15 -u -H {args.heuristic} beam_width={W} '
+            'data': f'synthetic: seeded solve trajectory (random.seed({args.seed})); timed: the saturated turns '
+                    f'{first}..{first + length - 1} of the {turns}-move goal-{GOAL} solve, replayed on '
+                    f'{win.engines} seeded solves set up outside the timed region',
+            'config': {'workload': f'speedrun goal_pts={GOAL} -u -H {args.heuristic} beam_width={W} '
                                    f'({args.width} per GPU; C5 at 8 GPUs x 4M)',
                        'beam_width': W, 'heuristic': args.heuristic, 'seed': args.seed,
                        'parallelism': f'beam sharded over {world} GPUs ({backend})',
-                       'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3)},
+                       'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
+                       'timed_turns': [first, first + length - 1], 'moves': turns},
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
             'cpu_baseline': None,
         }
+        if not args.no_cpu_baseline:   # after the timed region; the other ranks wait at the barrier below
+            out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, min(args.cpu_budget_s, 20.0))
         sys.stdout.flush()
         os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)
-    b.close()
+    dist.barrier()
     dist.destroy_process_group()

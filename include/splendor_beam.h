@@ -53,7 +53,8 @@ typedef struct {
     int32_t heuristic;         /* SB_HEUR_*; unknown names map to simple on the host (:429) */
     int32_t device;            /* HIP device ordinal */
     int64_t beam_width;        /* State.solve(beam_width)              src/solver.py:396 */
-    int32_t visited_log2;      /* log2 visited-set capacity (entries); 0 = auto from beam_width */
+    int32_t visited_log2;      /* log2 initial visited-set capacity (entries, 10..34); 0 = auto from beam_width and
+                                  free HBM; grown between turns either way (sb_visited_capacity) */
     int32_t flags;             /* bit 0: collect per-kernel timings; bit 1: sharded (sbd_*) mode even at world_size 1;
                                   bit 2 (test): generic first select pass instead of the one folded into the
                                   emission; bit 3 (test): folded pass with its window forced off the keys
@@ -121,6 +122,12 @@ int sb_sync(sb_engine* e);
 
 /* Visited-set entries (len(trail)). */
 int sb_visited_size(sb_engine* e, uint64_t* out);
+
+/* Visited-set capacity in slots and how often it was rebuilt larger.  The reference's trail is an
+ * unbounded dict (src/solver.py:425-426,447-450): before a turn whose worst case (every raw child new)
+ * could pass 60% load, the table is rehashed into 2^k times the slots while free HBM allows; results
+ * do not depend on the capacity.  Sharded mode: this rank's owner shard. */
+int sb_visited_capacity(sb_engine* e, uint64_t* capacity, int32_t* rebuilds);
 
 void sb_destroy(sb_engine* e);
 const char* sb_last_error(void);

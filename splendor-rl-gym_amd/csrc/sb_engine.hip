@@ -194,6 +194,32 @@ __global__ void k_insert_root(Entry* tab, uint64_t mask, uint64_t key) {
     tab[h].tag = 0;   // turn prefix 0: in trail before the first step
 }
 
+// ------------------------------------------------------------------ visited-set growth
+// The reference's `trail` is an unbounded dict (src/solver.py:425-426,447-450).  Between turns (no claim
+// in flight) a table whose next turn could push it past GROW_LOAD is rebuilt at 2^k times the slots:
+// every entry is re-inserted with its key AND tag, so the first-occurrence claims of later turns see
+// exactly the set they would have seen (results do not depend on the capacity; tests/test_gpu_growth.py).
+// Coalesced 16-B reads of the old table, one tag CAS + key store per entry into the new one.
+__global__ __launch_bounds__(256) void k_rehash(const Entry* __restrict__ old, uint64_t n_old, Entry* __restrict__ neu,
+                                                uint64_t mask, uint32_t* __restrict__ err) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_old; i += (uint64_t)gridDim.x * blockDim.x) {
+        const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&old[i]);
+        if (e.y == EMPTY) continue;
+        uint64_t h = mix64(e.x) & mask;
+        for (int probe = 0;; probe++) {
+            if (atomicCAS((unsigned long long*)&neu[h].tag, (unsigned long long)EMPTY, (unsigned long long)e.y) == EMPTY) {
+                neu[h].key = e.x;   // visible to the next turn's kernels (kernel boundary)
+                break;
+            }
+            h = (h + 1) & mask;
+            if (probe >= MAX_PROBE) {
+                atomicOr(err, 1u);
+                break;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ k_expand
 // tuning knobs (overridable with -D for experiments; see profiles/variants.sh)
 #ifndef SB_XP_PAR
@@ -675,9 +701,9 @@ struct Engine {
     DBuf<uint32_t> cnt, off;
     DBuf<uint64_t> nlo, nhi, skey;
     DBuf<uint32_t> npar, kidx;
-    uint32_t* d_small = nullptr;            // [0] n_unique total  [1] err  [2..8) claim stats ; [8..8+256) first-rank table ; [264] k_expand group counter
+    uint32_t* d_small = nullptr;            // [0] n_unique total  [1] err  [2..8) claim stats ; [8..8+256) first-rank table ; [264] k_expand group counter ; [266..268) u64 sharded owner key count
     unsigned long long* d_nraw = nullptr;
-    uint32_t* h_small = nullptr;            // pinned mirror of d_small (264 words)
+    uint32_t* h_small = nullptr;            // pinned mirror of d_small (272 words)
     unsigned long long* h_nraw = nullptr;
     ScanScratch scan;
     TopkScratch topk;
@@ -713,7 +739,50 @@ struct Engine {
     int dsel_npos = 1;                    // joint select: positions (histogram rows)
     DBuf<uint64_t> rkey;                  // sharded receive: keys of the received records
     DBuf<uint8_t> digit;
+    // visited-set growth (grow_table): largest raw children per parent seen so far, tables rebuilt
+    double raw_ratio = 32.0;
+    int n_grow = 0;
+    uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
 };
+
+// Visited-set capacity policy.  A table is rebuilt larger before a turn whose worst case (every raw
+// child a new key) could take it past GROW_LOAD; the size doubles while the free HBM allows (old and
+// new coexist during the rehash, GROW_RESERVE kept free for the step buffers).  If no larger table
+// fits, the old one stays and the HARD_LOAD check after the turn is the capacity limit.
+constexpr double GROW_LOAD = 0.6;
+constexpr double HARD_LOAD = 0.85;
+constexpr size_t GROW_RESERVE = (size_t)4 << 30;
+
+static void grow_table(Engine& E, Entry*& tab, uint64_t& mask, double projected) {
+    const uint64_t cap = mask + 1;
+    uint64_t ncap = cap;
+    while (projected > GROW_LOAD * (double)ncap && ncap < (1ull << 36)) ncap <<= 1;
+    if (ncap == cap) return;
+    size_t freeb = 0, totalb = 0;
+    SB_HIP(hipMemGetInfo(&freeb, &totalb));
+    while (ncap > cap && ncap * sizeof(Entry) + GROW_RESERVE > freeb) ncap >>= 1;
+    if (ncap == cap) return;
+    Entry* nt = nullptr;
+    SB_HIP(hipMalloc((void**)&nt, ncap * sizeof(Entry)));
+    SB_HIP(hipMemsetAsync(nt, 0xFF, ncap * sizeof(Entry), E.s));
+    hipLaunchKernelGGL(k_rehash, dim3(grid_cap((int64_t)std::min<uint64_t>(cap, 1ull << 40), 256, 1u << 16)), dim3(256), 0,
+                       E.s, tab, cap, nt, ncap - 1, E.d_small + 1);
+    SB_HIP(hipGetLastError());
+    SB_HIP(hipStreamSynchronize(E.s));
+    SB_HIP(hipFree(tab));
+    tab = nt;
+    mask = ncap - 1;
+    E.n_grow++;
+}
+
+// initial capacity (log2 entries) when visited_log2 = 0: `want` entries, at most a third of the free HBM
+static int auto_visited_log2(double want) {
+    size_t freeb = 0, totalb = 0;
+    SB_HIP(hipMemGetInfo(&freeb, &totalb));
+    int lg = 20;
+    while ((double)(1ull << lg) < want && lg < 34 && (double)(2ull << lg) * sizeof(Entry) <= (double)freeb / 3.0) lg++;
+    return lg;
+}
 
 static void check_err_word(Engine& E) {
     uint32_t e = E.h_small[1];
@@ -795,6 +864,8 @@ static void launch_front(Engine& E) {
     Turn& cur = E.turns.back();
     const int64_t n = cur.n;
     hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
+    // the claims below must fit: worst case every raw child is a new key
+    grow_table(E, E.tab, E.tab_mask, (double)E.visited + E.raw_ratio * (double)n);
     E.cand.ensure((size_t)n * 3);
     E.lost.ensure((size_t)n * 3);
     E.cnt.ensure((size_t)n);
@@ -888,8 +959,9 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     out->n_raw = (int64_t)*E.h_nraw;
     out->n_unique = nu;
     E.visited += (uint64_t)nu;
-    if ((double)E.visited > 0.85 * (double)(E.tab_mask + 1))
-        throw HipError{hipErrorOutOfMemory, "visited set above 85% load; raise visited_log2"};
+    if (n > 0) E.raw_ratio = std::max(E.raw_ratio, (double)out->n_raw / (double)n);
+    if ((double)E.visited > HARD_LOAD * (double)(E.tab_mask + 1))
+        throw HipError{hipErrorOutOfMemory, "visited set above 85% load and no larger table fits in free HBM"};
     if (nu == 0) {   // the queue empties: `puzzle` is the last parent expanded (src/solver.py:438,459)
         E.done = true;
         E.winner_rank = n - 1;
@@ -1100,13 +1172,9 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         for (auto& e : E.ev) SB_HIP(hipEventCreate(&e));
         E.d_tables = upload_tables(E.s);
         int lg = cfg->visited_log2;
-        if (lg <= 0) {
-            // ~10 unique children per parent per turn, ~20 turns, <= 50% load
-            double want = (double)cfg->beam_width * 10.0 * 20.0 * 2.0 / (cfg->world_size > 1 ? cfg->world_size : 1);
-            lg = 20;
-            while ((double)(1ull << lg) < want && lg < 31) lg++;
-        }
-        if (lg < 10 || lg > 32) throw HipError{hipErrorInvalidValue, "visited_log2 out of range [10, 32]"};
+        if (lg <= 0)   // ~10 unique children per parent per turn, ~20 turns, <= 50% load; grown past that
+            lg = auto_visited_log2((double)cfg->beam_width * 10.0 * 20.0 * 2.0 / (cfg->world_size > 1 ? cfg->world_size : 1));
+        if (lg < 10 || lg > 34) throw HipError{hipErrorInvalidValue, "visited_log2 out of range [10, 34]"};
         const uint64_t cap = 1ull << lg;
         const bool distm = cfg->world_size > 1 || (cfg->flags & 2);   // bit 1: sharded protocol at any world size
         const uint64_t tcap = distm ? 1024 : cap;   // sharded: the trail lives in the owner shards (E.own)
@@ -1122,9 +1190,9 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         }
         SB_HIP(hipMalloc((void**)&E.d_small, 272 * 4));
         SB_HIP(hipMalloc((void**)&E.d_nraw, 8));
-        SB_HIP(hipHostMalloc((void**)&E.h_small, 264 * 4, hipHostMallocDefault));
+        SB_HIP(hipHostMalloc((void**)&E.h_small, 272 * 4, hipHostMallocDefault));
         SB_HIP(hipHostMalloc((void**)&E.h_nraw, 8, hipHostMallocDefault));
-        SB_HIP(hipMemsetAsync(E.d_small, 0, 264 * 4, E.s));
+        SB_HIP(hipMemsetAsync(E.d_small, 0, 272 * 4, E.s));
         // root: turn 0, visited = {root}
         Turn t0;
         t0.lo = (uint64_t*)E.turn_mem.alloc(8);
@@ -1287,6 +1355,14 @@ int sb_sync(sb_engine* h) {
 int sb_visited_size(sb_engine* h, uint64_t* out) {
     if (!h || !out) return SB_ERR_ARG;
     *out = h->E.visited;
+    return SB_OK;
+}
+
+int sb_visited_capacity(sb_engine* h, uint64_t* capacity, int32_t* rebuilds) {
+    if (!h || !capacity || !rebuilds) return SB_ERR_ARG;
+    const Engine& E = h->E;
+    *capacity = (E.own ? E.own_mask : E.tab_mask) + 1;
+    *rebuilds = E.n_grow;
     return SB_OK;
 }
 

@@ -591,6 +591,10 @@ class HipBackend:
         self._chk(self.lib.sb_get_mt_state(self.h, out), 'sb_get_mt_state')
         return out
 
+    def visited_capacity(self) -> tuple[int, int]:
+        """(slots, rebuilds) of this rank's owner shard of the visited set."""
+        return self.L.visited_capacity(self.h)
+
     # ---------------------------------------------------------------- step primitives
     def expand(self, off, turn, world, nchunk=1):
         C = self.C

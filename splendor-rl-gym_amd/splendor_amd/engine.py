@@ -109,6 +109,10 @@ class BeamEngine:
         L.check(L.lib().sb_visited_size(self._h, C.byref(v)))
         return v.value
 
+    def visited_capacity(self) -> tuple[int, int]:
+        """(slots, rebuilds): the visited set grows between turns (include/splendor_beam.h)."""
+        return L.visited_capacity(self._h)
+
 
 def device_successors(lo, hi, device: int = 0):
     """Ordered successors of a batch of packed states on the GPU (the k_expand enumeration)."""

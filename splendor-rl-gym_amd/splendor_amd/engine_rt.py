@@ -99,6 +99,10 @@ class RealisticEngine:
     def path(self):
         return [unpack_state(w, self.config, self.tiers0, t) for t, w in enumerate(self.path_words())]
 
+    def visited_capacity(self) -> tuple[int, int]:
+        """(slots, rebuilds) of the visited set (grown between turns)."""
+        return L.visited_capacity(self._h)
+
     def mt_state(self):
         out = np.zeros(625, np.uint32)
         L.check(L.lib().sb_get_mt_state(self._h, out))

@@ -48,7 +48,7 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     st = random.getstate()[1]
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
-                   heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st)
+                   heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st, visited_log2=cfg.get('vlog2', 0))
     solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
     trace = solve.run()
     slices = []
@@ -57,7 +57,7 @@ def _worker(rank, world, port, cfg, outdir):
         rows = [b.turn_state(t, r) for r in range(n)]
         slices.append([[x[0] for x in rows], [x[1] for x in rows], [x[2] for x in rows]])
     out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'slices': slices,
-           'mt': b.mt_state().tolist()}
+           'mt': b.mt_state().tolist(), 'visited': list(b.visited_capacity())}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     b.close()
@@ -75,6 +75,8 @@ CASES = [
     (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3}),
     # four ranks on the one GPU (the driver's scaling runs use 2, 4 and 8 GPUs)
     (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'chunks': 2}),
+    # owner shards from a 1024-slot table: rebuilt larger between turns (unbounded trail)
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10}),
 ]
 
 
@@ -101,4 +103,6 @@ def test_sharded_engine_matches_oracle(world, cfg):
     assert [tuple(p) for p in res[0]['path']] == o.path()
     if cfg['heur']:
         assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    if 'vlog2' in cfg:
+        assert all(r['visited'][1] >= 2 and r['visited'][0] > (1 << cfg['vlog2']) for r in res), res[0]['visited']
     o.close()

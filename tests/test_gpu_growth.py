@@ -1,0 +1,65 @@
+"""Visited-set growth (the reference's `trail` is an unbounded dict, src/solver.py:425-426,447-450).
+
+Each engine starts from a deliberately tiny table (visited_log2) so that it is rebuilt larger several
+times between turns; every turn's beam (keys AND parent links), the path and the final MT19937 state
+must still equal the C oracle's — the capacity never changes a result.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_c
+from splendor_amd.engine import HEURISTIC_IDS, BeamEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _stepwise(eng, ora):
+    t = 0
+    while True:
+        a, b = eng.step(), ora.step()
+        for k in ('n_parents', 'n_raw', 'n_unique', 'n_kept', 'done', 'winner_rank', 'records'):
+            assert a[k] == b[k], (t, k, a[k], b[k])
+        if a['done']:
+            return t
+        t += 1
+        got, exp = eng.read_turn(t), ora.turn_arrays(t)
+        assert np.array_equal(got[-1], exp[-1]) and np.array_equal(got[-2], exp[-2]), f'turn {t}'
+
+
+@pytest.mark.parametrize('goal,heur,width,seed,vlog2', [(8, 'balanced', 20000, 7, 12), (9, 'efficiency', 3000, 8, 10),
+                                                         (6, 'simple', 500, 9, 10)])
+def test_speedrun_growth_vs_oracle(goal, heur, width, seed, vlog2):
+    random.seed(seed)
+    st = random.getstate()[1]
+    eng = BeamEngine(goal_pts=goal, use_heuristic=True, heuristic=HEURISTIC_IDS[heur], beam_width=width,
+                     mt_state625=st, visited_log2=vlog2)
+    ora = oracle_c.OracleSolve(goal, use_heuristic=True, heuristic_name=heur, beam_width=width, mt_state625=st)
+    _stepwise(eng, ora)
+    assert eng.path() == ora.path()
+    assert np.array_equal(eng.mt_state(), ora.mt_state())
+    cap, rebuilds = eng.visited_capacity()
+    assert rebuilds >= 2 and cap > (1 << vlog2), (cap, rebuilds)
+    assert eng.visited_size() <= 0.6 * cap
+    eng.close()
+    ora.close()
+
+
+def test_realistic_growth_vs_oracle():
+    from splendor_amd.engine_rt import RealisticEngine
+    from splendor_amd.realistic import GameConfig, MultiPlayerState, game_params, pack_state
+    cfg = GameConfig(num_players=2, target_points=7, gems_per_color=4, infinite_resources=False)
+    root = MultiPlayerState.newgame(cfg, shuffle_market=True, seed=11)
+    random.seed(11)
+    st = random.getstate()[1]
+    eng = RealisticEngine(root, beam_width=4000, mt_state625=st, visited_log2=10)
+    params, tiers = game_params(root.config, eng.tiers0)
+    o = oracle_c.OracleRealistic(params, tiers, beam_width=4000, mt_state625=st, root_w=pack_state(root, eng.tiers0))
+    _stepwise(eng, o)
+    assert np.array_equal(eng.path_words(), o.path())
+    assert np.array_equal(eng.mt_state(), o.mt_state())
+    cap, rebuilds = eng.visited_capacity()
+    assert rebuilds >= 2 and cap > 1024, (cap, rebuilds)
+    eng.close()
+    o.close()
