@@ -7,6 +7,8 @@ larger beam widths and stores the same trace format as tests/golden/make_golden.
 n_unique / n_kept / beam digest, solution path, final MT fingerprint).  Test infrastructure only.
 
     python3 oracle/make_big_golden.py --goal 15 --heur balanced --width 4000000 --seed 0
+    python3 oracle/make_big_golden.py --goal 15 --heur efficiency --width 4000000 --seed 0
+    python3 oracle/make_big_golden.py --realistic --goal 15 --width 1000000 --seed 0   # C4 (2 players, shuffled)
 """
 import argparse
 import json
@@ -25,10 +27,15 @@ from splendor_amd.solver import State  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--goal', type=int, required=True)
-    ap.add_argument('--heur', required=True)
+    ap.add_argument('--heur', default='balanced')
+    ap.add_argument('--realistic', action='store_true',
+                    help='MultiPlayerState (src/solver.py:750-860), competitive heuristic, shuffled market')
+    ap.add_argument('--players', type=int, default=2)
     ap.add_argument('--width', type=int, required=True)
     ap.add_argument('--seed', type=int, default=0)
     a = ap.parse_args()
+    if a.realistic:
+        return realistic(a)
     random.seed(a.seed)
     st = random.getstate()[1]
     o = oracle_c.OracleSolve(a.goal, use_heuristic=True, heuristic_name=a.heur, beam_width=a.width, mt_state625=st)
@@ -54,6 +61,43 @@ def main():
            'turns': turns, 'final_mt': oracle_c.mt_fingerprint(o.mt_state()), 'visited': o.visited_size(),
            'wall_s': round(time.time() - t0, 1)}
     name = f'oracle_g{a.goal}_{a.heur}_w{a.width}_s{a.seed}.json'
+    with open(os.path.join(os.path.dirname(HERE), 'tests', 'golden', name), 'w') as f:
+        json.dump(out, f, separators=(',', ':'))
+    print('wrote', name, out['moves'], 'moves', out['wall_s'], 's')
+
+
+def realistic(a):
+    """C4-style golden: the realistic oracle's per-turn digests, the path as packed words, the final MT."""
+    import numpy as np
+    from splendor_amd.engine_rt import device_tiers
+    from splendor_amd.realistic import GameConfig, MultiPlayerState, game_params, pack_state
+    cfg = GameConfig(num_players=a.players, target_points=a.goal, gems_per_color={2: 4, 3: 5, 4: 7}[a.players],
+                     infinite_resources=False)
+    root = MultiPlayerState.newgame(cfg, shuffle_market=True, seed=a.seed)
+    tiers0 = device_tiers(root)
+    params, tiers = game_params(cfg, tiers0)
+    random.seed(a.seed)
+    o = oracle_c.OracleRealistic(params, tiers, beam_width=a.width, mt_state625=random.getstate()[1],
+                                 root_w=pack_state(root, tiers0))
+    turns = []
+    t0 = time.time()
+    t = 0
+    while True:
+        ts = time.time()
+        r = o.step()
+        if r['done']:
+            break
+        t += 1
+        _, _, key = o.turn_arrays(t)
+        turns.append({'n_parents': r['n_parents'], 'n_raw': r['n_raw'], 'n_unique': r['n_unique'],
+                      'n_kept': r['n_kept'], 'digest': oracle_c.beam_digest(key), 's': round(time.time() - ts, 2)})
+        print(t, turns[-1], flush=True)
+    path = o.path()
+    out = {'goal': a.goal, 'players': a.players, 'shuffle': True, 'beam_width': a.width, 'seed': a.seed,
+           'source': 'oracle_c (realistic)', 'moves': len(path) - 1, 'winner_rank': r['winner_rank'],
+           'path_words': [[f'{int(x):016x}' for x in row] for row in np.asarray(path)],
+           'turns': turns, 'final_mt': oracle_c.mt_fingerprint(o.mt_state()), 'wall_s': round(time.time() - t0, 1)}
+    name = f'oracle_realistic_g{a.goal}_p{a.players}_shuf_w{a.width}_s{a.seed}.json'
     with open(os.path.join(os.path.dirname(HERE), 'tests', 'golden', name), 'w') as f:
         json.dump(out, f, separators=(',', ':'))
     print('wrote', name, out['moves'], 'moves', out['wall_s'], 's')
