@@ -41,6 +41,8 @@ extern "C" {
 #define SB_HEUR_BALANCED 1   /* balanced_heuristic    src/solver.py:218-249 (also 'competitive', :289-296) */
 #define SB_HEUR_AGGRESSIVE 2 /* aggressive_heuristic  src/solver.py:252-262 */
 #define SB_HEUR_EFFICIENCY 3 /* efficiency_heuristic  src/solver.py:265-286 */
+#define SB_HEUR_HOST 15      /* any other HEURISTICS callable (HEURISTICS.md:204-229, src/solver.py:299-305,429):
+                                the caller scores next_queue itself (sb_read_next + sb_prune) */
 
 #define SB_N_POW_EXP 11      /* exponents {0.3,0.4,0.5,0.6,0.7,0.8,1.2,2.0,2.5,2.8,3.2} */
 #define SB_POW_BASES 256     /* integer bases 0..255 */
@@ -96,6 +98,17 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
  * launched before returning (it overlaps the caller's work); the stats' device times are filled by
  * sb_turn_times once a turn has completed. */
 int sb_step(sb_engine* e, sb_step_stats* out);
+
+/* Host-scored turns (cfg.heuristic == SB_HEUR_HOST, use_heuristic = 1): sb_step runs the goal check, the
+ * expansion and the trail dedup, writes next_queue and returns with n_unique set and n_kept = 0 (or done);
+ * the caller reads next_queue (sb_read_next: states in next_queue order, the order `sorted` calls its key in,
+ * src/solver.py:453), scores every entry with its Python callable and hands the scores to sb_prune, which
+ * runs the stable descending top-k (`sorted(..., reverse=True)[:beam_width]`, ties in next_queue order) on
+ * the device, writes the next beam and launches the next expansion.  Scores are compared as f64 (-0.0 ==
+ * 0.0); a NaN fails the call (SB_ERR_HIP). *n_kept = len(queue) of the next turn.  sb_step is refused
+ * (SB_ERR_STATE) while a host-scored turn awaits sb_prune. */
+int sb_read_next(sb_engine* e, int64_t start, int64_t n, uint64_t* lo, uint64_t* hi);
+int sb_prune(sb_engine* e, const double* scores, int64_t n, int64_t* n_kept);
 
 /* Device phase times (ms) of a completed turn, timing flag set (flags bit 0): expand, count+scan,
  * host gap, emit, top-k, gather, total.  Speedrun handles only; the last 64 turns are kept. */

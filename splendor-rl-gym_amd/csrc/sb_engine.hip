@@ -65,13 +65,30 @@ constexpr int MAX_PROBE = 4096;
 // losing CAS attempts store here (see probe_insert); spread over 256 lines so they do not serialise
 __device__ unsigned long long g_claim_sink[4096];
 
+// Probe loads of the visited set.  -DSB_PROBE_NT=1 makes them non-temporal (global_load_dwordx4 ... nt):
+// alone, a random 16-B nt probe of a 32 GiB table runs at the cache-resident rate (54 G/s against 48 G/s,
+// profiles/micro/r2_randaccess2.txt), but inside k_expand it is 33% slower (expand 3.42 -> 4.56 ms,
+// profiles/r2_ab_probe_nt.txt): the probe's plain load leaves the line where the tag CAS that follows on
+// the same line finds it.  Plain loads are the default.
+#ifndef SB_PROBE_NT
+#define SB_PROBE_NT 0
+#endif
+__device__ __forceinline__ ulonglong2 load_entry(const Entry* __restrict__ e) {
+#if SB_PROBE_NT
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(e);
+    return make_ulonglong2(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1));
+#else
+    return *reinterpret_cast<const ulonglong2*>(e);
+#endif
+}
+
 template <bool PRE>
 __device__ __forceinline__ int probe_insert(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
                                             uint64_t tag, uint64_t& h, uint64_t& cur, uint32_t* err) {
     h = mix64(key) & mask;
     int wait = 0;
     for (int probe = 0;;) {
-        if (!PRE || probe > 0 || wait > 0) ent = *reinterpret_cast<const ulonglong2*>(&tab[h]);   // key and tag, one load
+        if (!PRE || probe > 0 || wait > 0) ent = load_entry(&tab[h]);   // key and tag, one load
         uint64_t k = ent.x, tg = ent.y;
 #ifndef SB_KEY_FIRST
         if (tg == EMPTY) {
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             }
 #pragma unroll
             for (int u = 0; u < XP_U; u++)
-                if (e[u] != 0xFFFFFFFFu) ent[u] = *reinterpret_cast<const ulonglong2*>(&tab[mix64(key[u]) & mask]);
+                if (e[u] != 0xFFFFFFFFu) ent[u] = load_entry(&tab[mix64(key[u]) & mask]);
 #pragma unroll
             for (int u = 0; u < XP_U; u++) {
                 if (e[u] == 0xFFFFFFFFu) continue;
@@ -743,6 +760,8 @@ struct Engine {
     double raw_ratio = 32.0;
     int n_grow = 0;
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
+    int64_t pending_host = -1;
+    double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
 
 // Visited-set capacity policy.  A table is rebuilt larger before a turn whose worst case (every raw
@@ -790,6 +809,7 @@ static void check_err_word(Engine& E) {
     if (e & 2u) throw HipError{hipErrorInvalidValue, "saved >= 256 exceeds the pow tables"};
     if (e & 4u) throw HipError{hipErrorLaunchFailure, "top-k sort look-back wait exceeded its bound"};
     if (e & 8u) throw HipError{hipErrorLaunchFailure, "sharded answers do not match the parents' move counts"};
+    if (e & 16u) throw HipError{hipErrorInvalidValue, "heuristic returned NaN: no stable sort order exists"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -895,6 +915,22 @@ static void launch_front(Engine& E) {
     E.front_turn = E.turn;
 }
 
+static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const double* host_scores, sb_step_stats* out);
+static double host_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// f64 scores of a host heuristic -> u64 keys whose unsigned order is the scores' order (-0.0 == 0.0 as in
+// Python's comparisons); a NaN has no place in that order (sorted() would not be a total order): error bit 16
+__global__ void k_order_keys(uint64_t* __restrict__ k, int64_t n, uint32_t* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t b = k[i];
+        if ((b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) atomicOr(err, 16u);
+        if (b == 0x8000000000000000ull) b = 0;
+        k[i] = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    }
+}
+
 static void engine_step(Engine& E, sb_step_stats* out) {
     memset(out, 0, sizeof *out);
     out->turn = E.turn;
@@ -908,11 +944,9 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     const int64_t n = cur.n;
     out->n_parents = n;
     if (E.front_turn != E.turn) launch_front(E);
-    static const bool htrace = getenv("SB_HOST_TRACE") != nullptr;
-    auto hnow = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    const double h0 = hnow();
+    E.htr[0] = host_ms();
     SB_HIP(hipStreamSynchronize(E.s));
-    const double h1 = hnow();
+    E.htr[1] = host_ms();
     E.front_turn = -1;
     // ---- goal check and max_pts records, in queue order (src/solver.py:438-445)
     const uint32_t* first = E.h_small + 8;
@@ -955,6 +989,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
             E.turn, E.h_small[2], E.h_small[3], E.h_small[4], E.h_small[5], E.h_small[6], E.h_small[7]);
 #endif
     const bool heur = E.cfg.use_heuristic != 0;
+    const bool host = heur && E.cfg.heuristic == SB_HEUR_HOST;   // scores from a host callable (sb_prune)
     const int64_t nu = E.h_small[0];
     out->n_raw = (int64_t)*E.h_nraw;
     out->n_unique = nu;
@@ -973,7 +1008,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     E.nlo.ensure(nu);
     E.nhi.ensure(nu);
     E.npar.ensure(nu);
-    if (heur) {
+    if (heur && !host) {
         E.skey.ensure(nu);
         const auto t0 = std::chrono::steady_clock::now();
         noise_ensure(E.noise, (uint64_t)nu, E.s_mt);
@@ -982,11 +1017,11 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     }
     hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
     if (timing) SB_HIP(hipEventRecord(ev[3], E.s));
-    const double h2 = hnow();
+    E.htr[2] = host_ms();
     const unsigned eg = grid_cap(n, 256, 8192);
     const uint64_t rbase = E.noise.consumed;
 #define EMIT_K(H) k_emit_w<H>
-    if (!heur) {
+    if (!heur || host) {   // full states + parent links, no scores
         hipLaunchKernelGGL(EMIT_K(-1), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, E.lost.p,
                            E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase, 0u,
                            E.d_small + 1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
@@ -1016,13 +1051,37 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         E.noise.consumed += (uint64_t)nu;
     }
     if (timing) SB_HIP(hipEventRecord(ev[4], E.s));
+    if (host) {   // the turn ends in sb_prune, once the caller has scored next_queue (sb_read_next)
+        SB_HIP(hipGetLastError());
+        E.pending_host = nu;
+        out->n_kept = 0;
+        return;
+    }
+    finish_turn(E, nu, heur, heur, nullptr, out);
+}
+
+// The prune and the next beam (src/solver.py:452-457): stable descending top-k of the score keys (heur),
+// the kept states written as the next turn (rebuilt from descriptors when `desc`), then the next turn's
+// expansion is launched.  host_scores: caller-supplied f64 scores of next_queue (custom heuristics).
+static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const double* host_scores, sb_step_stats* out) {
+    const bool timing = E.cfg.flags & 1;
+    Turn& cur = E.turns.back();
+    const int64_t n = cur.n;
+    hipEvent_t* ev = timing ? tev(E, E.turn) : nullptr;
     // ---- prune + next beam
     int64_t m = nu;
     uint32_t* idx = nullptr;
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
-        m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true, E.d_small + 1,
-                             /*fused=*/!(E.cfg.flags & 4));
+        if (host_scores) {   // f64 scores -> order-preserving u64 keys (a NaN sets error bit 16)
+            SB_HIP(hipMemcpyAsync(E.skey.p, host_scores, (size_t)nu * 8, hipMemcpyHostToDevice, E.s));
+            hipLaunchKernelGGL(k_order_keys, dim3(grid_cap(nu, 256, 8192)), dim3(256), 0, E.s, E.skey.p, nu, E.d_small + 1);
+            m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/false,
+                                 E.d_small + 1, /*fused=*/false);
+        } else {
+            m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true,
+                                 E.d_small + 1, /*fused=*/!(E.cfg.flags & 4));
+        }
         idx = E.kidx.p;
     }
     if (timing) SB_HIP(hipEventRecord(ev[5], E.s));
@@ -1032,7 +1091,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     nt.par = (uint32_t*)E.turn_mem.alloc(m * 4);
     nt.n = m;
     SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
-    if (heur)   // emission wrote descriptors only: rebuild the kept states from their parents
+    if (desc)   // emission wrote descriptors only: rebuild the kept states from their parents
         hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
                            cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8);
     else
@@ -1044,16 +1103,17 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     E.turn++;
     out->n_kept = m;
     out->noise_draws = E.noise.consumed;
-    const double h3 = hnow();
+    static const bool htrace = getenv("SB_HOST_TRACE") != nullptr;
+    const double h3 = host_ms();
     launch_front(E);   // the next turn's expansion follows the gather on the stream
-    const double h4 = hnow();
+    const double h4 = host_ms();
     if (htrace)
         fprintf(stderr, "turn %d sync %.3f pre-emit %.3f back %.3f front %.3f | old %u ins %u dup_early %u dup_lost %u displaced %u\n",
-                E.turn, h1 - h0, h2 - h1, h3 - h2, h4 - h3, E.h_small[2], E.h_small[3], E.h_small[4], E.h_small[5],
-                E.h_small[6]);
+                E.turn, E.htr[1] - E.htr[0], E.htr[2] - E.htr[1], h3 - E.htr[2], h4 - h3, E.h_small[2], E.h_small[3],
+                E.h_small[4], E.h_small[5], E.h_small[6]);
     // noise for the next turns on the side stream, overlapping that (latency-bound) expansion:
     // keep about three steps of accepted draws ahead
-    if (heur && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n)
+    if (heur && !host_scores && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n)
         noise_generate_async(E.noise, E.s_mt);
 }
 
@@ -1246,9 +1306,62 @@ int sb_step(sb_engine* h, sb_step_stats* out) {
         set_error("sb_step: realistic handle (use sbr_step)");
         return SB_ERR_STATE;
     }
+    if (h->E.pending_host >= 0) {
+        set_error("sb_step: the previous turn awaits its host scores (sb_prune)");
+        return SB_ERR_STATE;
+    }
     return guarded([&]() {
         SB_HIP(hipSetDevice(h->E.dev));
         engine_step(h->E, out);
+        return SB_OK;
+    });
+}
+
+int sb_read_next(sb_engine* h, int64_t start, int64_t n, uint64_t* lo, uint64_t* hi) {
+    if (!h || h->E.pending_host < 0) {
+        set_error("sb_read_next: no host-scored turn pending");
+        return SB_ERR_STATE;
+    }
+    Engine& E = h->E;
+    if (start < 0 || n < 0 || start + n > E.pending_host) {
+        set_error("sb_read_next: range out of bounds");
+        return SB_ERR_ARG;
+    }
+    if (n == 0) return SB_OK;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(E.dev));
+        if (lo) SB_HIP(hipMemcpyAsync(lo, E.nlo.p + start, n * 8, hipMemcpyDeviceToHost, E.s));
+        if (hi) SB_HIP(hipMemcpyAsync(hi, E.nhi.p + start, n * 8, hipMemcpyDeviceToHost, E.s));
+        SB_HIP(hipStreamSynchronize(E.s));
+        return SB_OK;
+    });
+}
+
+int sb_prune(sb_engine* h, const double* scores, int64_t n, int64_t* n_kept) {
+    if (!h || !scores || !n_kept) {
+        set_error("sb_prune: null argument");
+        return SB_ERR_ARG;
+    }
+    Engine& E = h->E;
+    if (E.pending_host < 0) {
+        set_error("sb_prune: no host-scored turn pending");
+        return SB_ERR_STATE;
+    }
+    if (n != E.pending_host) {
+        set_error("sb_prune: one score per next_queue entry expected");
+        return SB_ERR_ARG;
+    }
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(E.dev));
+        sb_step_stats st;
+        memset(&st, 0, sizeof st);
+        E.skey.ensure((size_t)n);
+        E.htr[2] = host_ms();
+        E.pending_host = -1;
+        finish_turn(E, n, true, false, scores, &st);
+        SB_HIP(hipStreamSynchronize(E.s));   // the caller's score buffer is free on return
+        check_err_word(E);
+        *n_kept = st.n_kept;
         return SB_OK;
     });
 }

@@ -25,11 +25,12 @@ SB_ERR_HIP = -2
 SB_ERR_STATE = -3
 SB_ERR_CAPACITY = -4
 SB_ERR_NOTABLES = -5
+SB_HEUR_HOST = 15   # a Python HEURISTICS callable scores next_queue on the host (sb_read_next / sb_prune)
 
 # exponents of the host-captured pow tables, in SB row order (include/splendor_beam.h)
 POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
-EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_turn_times', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
+EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_read_next', 'sb_prune', 'sb_turn_times', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
             'sb_get_mt_state', 'sb_sync', 'sb_visited_size', 'sb_visited_capacity', 'sb_destroy', 'sb_last_error', 'sb_version',
             'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk',
             'sbd_goal_table', 'sbd_expand', 'sbd_pack', 'sbd_owner_begin', 'sbd_owner_claim', 'sbd_owner_finish', 'sbd_pack_bits', 'sbd_unpack_bits', 'sbd_apply', 'sbd_emit',
@@ -104,6 +105,8 @@ def lib():
         L.sb_init_tables.argtypes = [i32p, f64p, f64p]
         L.sb_create.argtypes = [C.POINTER(SbConfig), u32p, C.c_uint64, C.c_uint64, C.POINTER(vp)]
         L.sb_step.argtypes = [vp, C.POINTER(SbStepStats)]
+        L.sb_read_next.argtypes = [vp, C.c_int64, C.c_int64, vp, vp]
+        L.sb_prune.argtypes = [vp, vp, C.c_int64, C.POINTER(C.c_int64)]
         L.sb_turn_times.argtypes = [vp, C.c_int32, np.ctypeslib.ndpointer(np.float32, flags='C')]
         L.sb_num_turns.argtypes = [vp, C.POINTER(C.c_int32)]
         L.sb_turn_size.argtypes = [vp, C.c_int32, C.POINTER(C.c_int64)]

@@ -586,6 +586,17 @@ class HipBackend:
                   'sb_read_turn')
         return int(lo[0]), int(hi[0]), int(par[0])
 
+    def turn_keys(self, t: int) -> np.ndarray:
+        """State keys of this rank's slice of turn t (the slice in global queue order)."""
+        C = self.C
+        n = C.c_int64()
+        self._chk(self.lib.sb_turn_size(self.h, int(t), C.byref(n)), 'sb_turn_size')
+        key = np.zeros(n.value, np.uint64)
+        if n.value:
+            self._chk(self.lib.sb_read_turn(self.h, int(t), 0, n.value, None, None, None, key.ctypes.data),
+                      'sb_read_turn')
+        return key
+
     def mt_state(self) -> np.ndarray:
         out = np.zeros(625, np.uint32)
         self._chk(self.lib.sb_get_mt_state(self.h, out), 'sb_get_mt_state')

@@ -31,6 +31,8 @@ class BeamEngine:
         self._h = h
         self.done = False
         self.turn = 0
+        self.host_scored = bool(use_heuristic) and int(heuristic) == L.SB_HEUR_HOST
+        self.pending = 0
 
     def close(self):
         if getattr(self, '_h', None):
@@ -53,7 +55,26 @@ class BeamEngine:
         self.done = d['done']
         if not self.done:
             self.turn += 1
+        self.pending = d['n_unique'] if (self.host_scored and not self.done) else 0
         return d
+
+    def read_next(self, start: int = 0, n: int | None = None):
+        """next_queue of a host-scored turn (heuristic=SB_HEUR_HOST) after step(): packed (lo, hi) arrays."""
+        if n is None:
+            n = self.pending - start
+        lo = np.zeros(n, np.uint64)
+        hi = np.zeros(n, np.uint64)
+        L.check(L.lib().sb_read_next(self._h, int(start), int(n), lo.ctypes.data, hi.ctypes.data), 'sb_read_next')
+        return lo, hi
+
+    def prune(self, scores) -> int:
+        """Stable descending top-k of host scores over next_queue (sorted(..., reverse=True)[:beam_width]) on the
+        device; the next turn's beam is written and its expansion launched.  Returns the kept count."""
+        sc = np.ascontiguousarray(np.asarray(scores, dtype=np.float64))
+        kept = C.c_int64()
+        L.check(L.lib().sb_prune(self._h, sc.ctypes.data, len(sc), C.byref(kept)), 'sb_prune')
+        self.pending = 0
+        return kept.value
 
     def turn_times(self, t: int) -> dict:
         """Device phase times (ms) of completed turn t (engine created with timing=True)."""

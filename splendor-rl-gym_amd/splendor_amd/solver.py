@@ -16,6 +16,7 @@ from bisect import insort
 from collections.abc import Callable
 from random import randint
 
+from . import _lib as L
 from . import codec
 from .deck import COLOR_NUM, MAX_GEMS, Color, get_deck
 from .engine import HEURISTIC_IDS, BeamEngine, device_successors
@@ -156,7 +157,9 @@ class State:
 
         Same signature, output and printing as the reference; ``device`` picks the
         GPU; ``sync_random`` leaves Python's ``random`` where the reference would
-        (after one ``randint`` per scored state).
+        (after one ``randint`` per scored state).  A heuristic registered in
+        ``HEURISTICS`` by the user runs as Python on the host over the device's
+        next_queue (see ``_host_scores``); the built-in ones run on the device.
         """
         if verbose:
             print('=' * 60)
@@ -171,11 +174,12 @@ class State:
             print('=' * 60)
             print()
         heuristic = HEURISTICS.get(heuristic_name, simple_heuristic)
-        hid = _BUILTIN_IDS.get(heuristic)
-        if hid is None:
-            raise NotImplementedError(
-                f'heuristic {heuristic_name!r} is a user Python callable; the MI355X engine evaluates only the '
-                f'built-in scorers {sorted(HEURISTIC_IDS)} on the device')
+        hid = _BUILTIN_IDS.get(heuristic, 0) if use_heuristic else 0
+        if use_heuristic and heuristic not in _BUILTIN_IDS:
+            # a user-registered callable (HEURISTICS.md:204-229): the device expands and dedups; the callable
+            # scores next_queue on the host, in next_queue order (the order `sorted` calls its key in, so it
+            # consumes `random` exactly as the reference); the device runs the stable top-k of its scores
+            hid = L.SB_HEUR_HOST
         st = random.getstate()
         lo, hi = self.packed()
         eng = BeamEngine(goal_pts=goal_pts, use_heuristic=use_heuristic, heuristic=hid, beam_width=beam_width,
@@ -191,14 +195,33 @@ class State:
                         print(f'max_pts={pts:<7} {State.from_packed(*eng.state_at(turn, rank))}')
                 if stats['done']:
                     break
+                if eng.host_scored:
+                    eng.prune(_host_scores(eng, heuristic))
                 turn += 1
             path = [State.from_packed(a, b) for a, b in eng.path()]
-            if use_heuristic and sync_random:
+            if use_heuristic and sync_random and not eng.host_scored:
                 mt = eng.mt_state()
                 random.setstate((st[0], tuple(int(x) for x in mt), st[2]))
         finally:
             eng.close()
         return path
+
+
+def _host_scores(eng: BeamEngine, heuristic, chunk: int = 1 << 20):
+    """The callable's score of every next_queue entry, in next_queue order, as float64.  Python compares the
+    returned values exactly; a value float64 cannot hold exactly (an int beyond 2**53) would be ordered
+    differently on the device, so it is refused."""
+    import numpy as np
+    out = np.empty(eng.pending, dtype=np.float64)
+    for a in range(0, eng.pending, chunk):
+        lo, hi = eng.read_next(a, min(chunk, eng.pending - a))
+        for i, (x, y) in enumerate(zip(lo.tolist(), hi.tolist())):
+            v = heuristic(State.from_packed(x, y))
+            f = float(v)
+            if type(v) is not float and f != v:
+                raise TypeError(f'heuristic returned {v!r}, which float64 cannot represent exactly')
+            out[a + i] = f
+    return out
 
 
 __all__ = ['State', 'HEURISTICS', 'simple_heuristic', 'balanced_heuristic', 'aggressive_heuristic',

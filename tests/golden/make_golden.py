@@ -15,6 +15,9 @@ Usage (from the repo root)::
     PYTHONPATH=/tmp/oracle_shim:/tmp/refcopy python3 tests/golden/make_golden.py tables
     PYTHONPATH=... python3 tests/golden/make_golden.py solve --goal 10 --heur simple --width 300000 --seed 0
 
+The reference's shipped buys.pickle is never unpickled: delete it from the copy first
+(``rm /tmp/refcopy/buys.pickle``), so the reference generates and pickles its own table.
+
 Digest convention (shared with ``oracle/`` and the engine): the digest of a beam
 is ``sha256(b''.join(struct.pack('<q', hash(s)) for s in beam)).hexdigest()[:16]``.
 """
@@ -213,6 +216,36 @@ def cmd_bfs(_args):
     _dump('bfs.json', out)
 
 
+def cmd_custom(_args):
+    """Seeded solves with user-registered heuristics (tests/custom_heuristics.py) added to HEURISTICS."""
+    import src.solver as S
+    sys.path.insert(0, os.path.dirname(HERE))
+    from custom_heuristics import CASES, CUSTOM
+    S.HEURISTICS.update(CUSTOM)
+    out = []
+    for goal, name, width, seed in CASES:
+        r = _run_speedrun(goal, name, width, seed)
+        print(goal, name, width, seed, r['moves'], r['wall_s'])
+        out.append(r)
+    _dump('solves_custom.json', out)
+
+
+def cmd_verbose(_args):
+    """stdout of the reference CLI (splendor_fastest_win.py) without -q, random.seed(0), each in a fresh process
+    (the reference's buys-table messages are whatever its first get_buys() prints in that process)."""
+    import subprocess
+    out = []
+    code = ('import random, sys; random.seed(0); sys.argv = ["splendor_fastest_win.py"] + sys.argv[1:]; '
+            'import splendor_fastest_win as F; F.cli()')
+    for argv in (['6', '-u', '-w', '1000'], ['4'], ['7', '-u', '-H', 'balanced', '-w', '500', '-r'],
+                 ['6', '--realistic', '-w', '3000'], ['5', '--realistic', '--players', '3', '-w', '400']):
+        r = subprocess.run([sys.executable, '-c', code, *argv], capture_output=True, text=True, cwd=REF_PATH,
+                           check=True)
+        out.append({'argv': argv, 'seed': 0, 'stdout': r.stdout})
+        print(argv, len(r.stdout.splitlines()), 'lines')
+    _dump('cli_verbose.json', out)
+
+
 def _mp_key(st):
     return st.hash
 
@@ -361,6 +394,8 @@ def main():
     sub.add_parser('realistic_small')
     sub.add_parser('realistic_inf_succ')
     sub.add_parser('realistic_inf_small')
+    sub.add_parser('custom')
+    sub.add_parser('verbose')
     p = sub.add_parser('solve')
     p.add_argument('--goal', type=int, required=True)
     p.add_argument('--heur', required=True)
@@ -374,7 +409,8 @@ def main():
     p.add_argument('--shuffle', action='store_true')
     args = ap.parse_args()
     {'tables': cmd_tables, 'solve': cmd_solve, 'solves_small': cmd_solves_small, 'bfs': cmd_bfs,
-     'realistic': cmd_realistic, 'realistic_succ': cmd_realistic_succ,
+     'realistic': cmd_realistic, 'realistic_succ': cmd_realistic_succ, 'custom': cmd_custom,
+     'verbose': cmd_verbose,
      'realistic_small': cmd_realistic_small, 'realistic_inf_succ': cmd_realistic_inf_succ,
      'realistic_inf_small': cmd_realistic_inf_small}[args.cmd](args)
 

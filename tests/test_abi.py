@@ -40,6 +40,8 @@ def test_argument_errors_without_gpu():
     L = _lib.lib()
     assert L.sb_step(None, None) == _lib.SB_ERR_ARG
     assert L.sb_sync(None) == _lib.SB_ERR_ARG
+    assert L.sb_read_next(None, 0, 0, None, None) == _lib.SB_ERR_STATE
+    assert L.sb_prune(None, None, 0, None) == _lib.SB_ERR_ARG
     cfg = _lib.SbConfig(goal_pts=3, use_heuristic=0, heuristic=0, device=0, beam_width=0)
     import numpy as np
     h = ctypes.c_void_p()

@@ -82,3 +82,21 @@ def test_cli_realistic_on_gpu():
     for pid, cards, _gems, _bonus, pts, _saved in g['final']:
         assert f'  Player {pid}: {pts} points, {len(cards)} cards' in out.stdout
     assert 'Move-by-move breakdown:' in out.stdout and f'Move {g["moves"]}: ' in out.stdout
+
+
+# the reference's lazy buys-table loader prints these on its first get_buys() (src/buys.py:25-36); the engine
+# tests affordability on the device and loads no table, so they are the one difference in the stdout
+_BUYS_MESSAGES = {'Unpickling buys...', 'Generating buys...', 'Pickling buys...', 'Pickling finished.'}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', range(5))
+def test_cli_verbose_output_matches_reference(case):
+    """Full stdout without -q (banner, turn= / max_pts= progress lines, realistic every-100-turns line, solution
+    or render) equals the reference CLI's under random.seed(0) (tests/golden/cli_verbose.json)."""
+    g = golden('cli_verbose.json')[case]
+    out = subprocess.run([sys.executable, SCRIPT, *g['argv'], '--seed', str(g['seed'])], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    exp = [ln for ln in g['stdout'].splitlines() if ln not in _BUYS_MESSAGES]
+    assert out.stdout.splitlines() == exp

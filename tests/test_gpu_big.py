@@ -1,0 +1,108 @@
+"""Parity at the benchmark configs' own widths (BASELINE.json configs[2..4]) against committed goldens of
+the pinned C oracle (oracle/make_big_golden.py; the Python reference cannot run these widths here):
+
+  * C4: realistic 2 players, goal 15, shuffled market seed 0, W=1M, one GPU
+  * the sharded protocol at W=4M: world 1 (flags bit 1) on C3 (balanced), and world 2 on one GPU (gloo
+    transport, HIP per-rank primitives) on C5's heuristic (efficiency) — every turn's beam digest over the
+    rank slices in rank order, turn sizes, path and final MT state
+"""
+import json
+import os
+import random
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_c
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_realistic_c4_w1m_oracle_golden():
+    from splendor_amd.engine_rt import RealisticEngine
+    from splendor_amd.realistic import GameConfig, MultiPlayerState
+    g = golden('oracle_realistic_g15_p2_shuf_w1000000_s0.json')
+    cfg = GameConfig(num_players=2, target_points=15, gems_per_color=4, infinite_resources=False)
+    root = MultiPlayerState.newgame(cfg, shuffle_market=True, seed=g['seed'])
+    random.seed(g['seed'])
+    eng = RealisticEngine(root, beam_width=g['beam_width'], mt_state625=random.getstate()[1])
+    t = 0
+    while True:
+        s = eng.step()
+        if s['done']:
+            break
+        t += 1
+        exp = g['turns'][t - 1]
+        assert (s['n_parents'], s['n_raw'], s['n_unique'], s['n_kept']) == \
+            (exp['n_parents'], exp['n_raw'], exp['n_unique'], exp['n_kept']), t
+        _, _, key = eng.read_turn(t)
+        assert oracle_c.beam_digest(key) == exp['digest'], f'turn {t}'
+    assert t == len(g['turns'])
+    words = eng.path_words()
+    assert [[f'{int(x):016x}' for x in row] for row in words] == g['path_words']
+    assert oracle_c.mt_fingerprint(eng.mt_state()) == g['final_mt']
+    eng.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from splendor_amd.dist import Comm, DistSolve, HipBackend
+    from splendor_amd.engine import HEURISTIC_IDS
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    random.seed(cfg['seed'])
+    b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=True,
+                   heuristic=HEURISTIC_IDS[cfg['heuristic']], beam_width=cfg['width'],
+                   mt_state625=random.getstate()[1])
+    solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=True, beam_width=cfg['width'])
+    trace = []
+    while True:
+        st = solve.step()
+        trace.append(st)
+        if st['done']:
+            break
+        np.save(os.path.join(outdir, f'keys_t{len(trace)}_r{rank}.npy'), b.turn_keys(len(trace)))
+    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist()}
+    with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
+        json.dump(out, f)
+    b.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,name', [(1, 'oracle_g15_balanced_w4000000_s0.json'),
+                                        (2, 'oracle_g15_efficiency_w4000000_s0.json')])
+def test_sharded_w4m_oracle_golden(world, name):
+    g = golden(name)
+    cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed']}
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
+        res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
+        turns = [t for t in res[0]['trace'] if not t['done']]
+        assert len(turns) == len(g['turns'])
+        for t, exp in enumerate(g['turns'], 1):
+            a = turns[t - 1]
+            assert (a['n_raw'], a['n_unique'], a['n_kept']) == (exp['n_raw'], exp['n_unique'], exp['n_kept']), t
+            key = np.concatenate([np.load(os.path.join(d, f'keys_t{t}_r{r}.npy')) for r in range(world)])
+            assert oracle_c.beam_digest(key) == exp['digest'], f'turn {t}'
+    from splendor_amd.codec import state_key, decode, to_signed
+    path = [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in res[0]['path']]
+    assert path == [p[5] for p in g['path']]
+    assert all(oracle_c.mt_fingerprint(r['mt']) == g['final_mt'] for r in res)

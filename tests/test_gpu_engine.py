@@ -194,6 +194,13 @@ def test_solve_c3_w4m_oracle_golden():
     _check_against_golden(g)
 
 
+def test_solve_efficiency_w4m_oracle_golden():
+    """C5's heuristic (efficiency) at C3's width on one GPU: the golden the sharded W=4M test also uses."""
+    g = golden('oracle_g15_efficiency_w4000000_s0.json')
+    assert g['moves'] == 15
+    _check_against_golden(g)
+
+
 def test_bfs_golden():
     for g in golden('bfs.json'):
         eng = BeamEngine(goal_pts=g['goal'], use_heuristic=False, heuristic=0, beam_width=1, mt_state625=_mt(0))
