@@ -197,7 +197,9 @@ __device__ __forceinline__ int take_bucket(const Derived& d) {
 template <int H>
 __device__ __forceinline__ double score_vals(const double (*pw)[POW_BASES], int pts, int saved, int G, int B, int U,
                                              double noise) {
-    saved = saved < POW_BASES ? saved : POW_BASES - 1;   // guarded on the host: saved < 256 asserted
+    // keeps the table read in bounds only: a state with saved >= 256 sets error bit 2 in the emission
+    // (sb_wave.inc) and sb_step fails with "saved >= 256 exceeds the pow tables" (tests: saved_overflow)
+    saved = saved < POW_BASES ? saved : POW_BASES - 1;
     if constexpr (H == 0) {   // simple
         return pw[P04][saved] * pw[P25][pts] + noise;
     } else if constexpr (H == 1) {   // balanced

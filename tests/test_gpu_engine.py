@@ -237,3 +237,17 @@ def test_vs_oracle_stepwise_random_configs():
         assert np.array_equal(eng.mt_state(), ora.mt_state())
         eng.close()
         ora.close()
+
+
+def test_saved_overflow_is_an_error_not_a_clamp():
+    """saved >= 256 is past the pow tables: the step fails loudly instead of scoring with a clamped value."""
+    from splendor_amd import _lib as L
+    from splendor_amd.codec import encode
+    lo, hi = encode((), (0, 0, 0, 0, 0), 0, 300)
+    eng = BeamEngine(goal_pts=15, use_heuristic=True, heuristic=1, beam_width=100, mt_state625=_mt(0),
+                     root_lo=lo, root_hi=hi)
+    eng.step()   # turn 0: the root's children are scored in this step's emission
+    with pytest.raises(L.SplendorBeamError, match='saved >= 256'):
+        for _ in range(3):
+            eng.step()
+    eng.close()
