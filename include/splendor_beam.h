@@ -167,8 +167,9 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
  * (sbd_set_stream); calls that return host values wait for it. ---- */
 /* local first rank per pts of this rank's queue slice (0xFFFFFFFF = none) */
 int sbd_goal_table(sb_engine* e, uint32_t* first256);
-/* expand the local slice (global queue offset goff): every successor becomes a record (key, owner =
- * fmix64(key) >> 40 mod world), stably partitioned by owner.  The records are cut into nchunk (<= 16)
+/* expand the local slice (global queue offset goff): the successors this rank owns (owner = fmix64(key)
+ * >> 40 mod world) are claimed in its shard of the visited set; every other successor becomes a record
+ * (key), stably partitioned by owner.  The records are cut into nchunk (<= 16)
  * exchange chunks of whole 4096-record tiles; chunk_owner_counts[nchunk][world] = records per chunk
  * and owner, *n_raw = successors generated */
 int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int32_t nchunk, int64_t* chunk_owner_counts,
@@ -176,12 +177,13 @@ int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int32_t nchunk, int64_
 /* the record keys grouped by owner, (parent, ordinal) order inside a group (d_tag unused: tags are
  * implicit in the order) */
 int sbd_pack(sb_engine* e, uint64_t* d_key, uint64_t* d_tag);
-/* owner side, per turn: begin(n_total records this owner receives), one claim per received chunk (in
- * any order: tags carry the global order), finish.  A chunk holds nseg source segments: source q's
- * records at [seg_start[q], seg_start[q+1]) (seg_start[0] = 0), global record indices seg_base[q]..
- * (source rank major, then parent order).  d_ret[global index] = 1 for a first occurrence, final
- * after sbd_owner_finish. */
-int sbd_owner_begin(sb_engine* e, int64_t n_total);
+/* owner side, per turn: begin(n_total records this owner receives; src_base[q] = answer index of source
+ * q's first record, nsrc = world), one claim per received chunk (in any order: tags carry the global
+ * order), finish.  A chunk holds nseg source segments: source q's records at [seg_start[q],
+ * seg_start[q+1]) (seg_start[0] = 0), answer indices seg_base[q].. (source rank major, then parent
+ * order).  d_ret[answer index] = 1 for a first occurrence, final after sbd_owner_finish.  The children a
+ * rank owns itself never become records: sbd_expand claims them in its shard. */
+int sbd_owner_begin(sb_engine* e, int64_t n_total, int32_t nsrc, const int64_t* src_base);
 int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, int64_t n, int32_t nseg, const int64_t* seg_start,
                     const int64_t* seg_base, uint8_t* d_ret);
 int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);

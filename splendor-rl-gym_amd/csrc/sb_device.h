@@ -254,6 +254,12 @@ __device__ __forceinline__ void buy_set(const uint64_t (*aff_lo)[8], const uint3
     *blo = ml;
     *bhi = mh;
 }
+// 192-bit move space of a parent: bit dsc set for every legal move (buys 0..89, takes NCARDS + bit)
+__device__ __forceinline__ void move_space(uint64_t bl, uint32_t bh, uint64_t t0, uint64_t t1, uint64_t* w) {
+    w[0] = bl;
+    w[1] = (uint64_t)bh | (t0 << (NCARDS - 64));
+    w[2] = (t0 >> (128 - NCARDS)) | (t1 << (NCARDS - 64));
+}
 // per-colour bonus counts packed 5 bits each
 __device__ __forceinline__ uint32_t pack_bonus(const Derived& d) {
     uint32_t p = 0;

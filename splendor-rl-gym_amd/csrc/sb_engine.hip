@@ -150,7 +150,18 @@ __device__ __forceinline__ int probe_insert(Entry* __restrict__ tab, uint64_t ma
 // claimant that lowers a same-turn tag marks the displaced holder in `lost`; one whose atomicMin finds
 // a smaller tag has lost itself.  Every duplicate is therefore resolved by exactly one of the two, and
 // once the grid drains the survivors are cand & ~lost — no second pass over the table.
-template <bool PRE>
+// Sharded tags (sb_dist.inc): (turn+1) << 40 | source rank << SH_Q_SHIFT | local order, the local order of
+// a child claimed by its own rank being (local parent rank << 8 | dsc) and of a record received from rank q
+// its index among q's records to this owner.  Ordered like the global (parent rank, ordinal) order.
+constexpr int SH_Q_SHIFT = 34;
+constexpr uint64_t SH_LOCAL_MASK = (1ull << SH_Q_SHIFT) - 1;
+constexpr uint64_t SH_RANK_MASK = (1ull << (SH_Q_SHIFT - 8)) - 1;   // local parent ranks < 2^26
+
+__host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
+    return (uint32_t)((mix64(key) >> 40) % world);
+}
+
+template <bool PRE, bool SH = false>
 __device__ __forceinline__ bool claim_lm(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
                                          uint64_t tag, unsigned long long* __restrict__ lost, uint32_t* err) {
     uint64_t h, cur = EMPTY;
@@ -175,7 +186,7 @@ __device__ __forceinline__ bool claim_lm(Entry* __restrict__ tab, uint64_t mask,
 #endif
     if (old < tag) return false;
     if (old != EMPTY) {   // old > tag >= this turn's prefix: a same-turn holder, now displaced
-        const uint64_t ro = (old >> 8) & 0xFFFFFFFFull;
+        const uint64_t ro = (old >> 8) & (SH ? SH_RANK_MASK : 0xFFFFFFFFull);
         const uint32_t oo = (uint32_t)(old & 255);
         atomicOr(&lost[ro * 3 + (oo >> 6)], 1ull << (oo & 63));
     }
@@ -188,9 +199,10 @@ __device__ __forceinline__ bool visit_claim_lm(Entry* __restrict__ tab, uint64_t
 }
 
 // visit_claim_lm with the entry at the key's home slot already loaded (ent)
+template <bool SH = false>
 __device__ __forceinline__ bool visit_claim_lm_pre(Entry* __restrict__ tab, uint64_t mask, uint64_t key, ulonglong2 ent,
                                                    uint64_t tag, unsigned long long* __restrict__ lost, uint32_t* err) {
-    return claim_lm<true>(tab, mask, key, ent, tag, lost, err);
+    return claim_lm<true, SH>(tab, mask, key, ent, tag, lost, err);
 }
 
 __device__ __forceinline__ uint64_t lookup_tag(const Entry* __restrict__ tab, uint64_t mask, uint64_t key) {
@@ -279,6 +291,7 @@ struct XpShared {
     uint16_t qb[XP_PAR * NCARDS];     // buy children (s | dsc << 5)
     uint16_t qt[XP_PAR * NPAT_MAX];   // take children: phase B runs all buys, then all takes, so a
     uint32_t nqb, nqt, nraw;          // wave rarely mixes the two (a buy re-hashes its card tuple)
+    uint32_t proff[XP_PAR];           // SH: first record of each parent
     uint32_t grp[3];                  // this, next and next-but-one parent group
 };
 
@@ -327,12 +340,19 @@ __device__ __forceinline__ void derive_lds(const uint64_t* mlo, const uint32_t* 
 // (turn, parent rank, dsc) orders exactly like (turn, parent rank, ordinal), and the candidate /
 // lost bits of a parent are indexed by dsc (the 192-bit move space of move_space()).
 // Displaced same-turn claims are marked in `lost` (lost marking).
+// SH (sharded step, sb_dist.inc): the children this rank owns (owner_of(key) == me) are claimed here in
+// its owner shard `tab` with tag (me, local rank, dsc); every other child becomes a record for its owner:
+// key and owner digit at roff[parent] + ordinal (digit 0xFF = claimed here), the layout the owner
+// partition reads.  cand / lost then hold the own children's claims only.
+template <bool SH>
 __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __restrict__ T, const uint64_t* __restrict__ blo,
                                                   const uint64_t* __restrict__ bhi, int64_t n, Entry* __restrict__ tab,
                                                   uint64_t mask, uint64_t turn_tag, unsigned long long* __restrict__ cand,
                                                   unsigned long long* __restrict__ lost,
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err,
-                                                  uint32_t* __restrict__ work) {
+                                                  uint32_t* __restrict__ work, uint32_t me, uint32_t world,
+                                                  const uint32_t* __restrict__ roff, uint64_t* __restrict__ rkey,
+                                                  uint8_t* __restrict__ rdig) {
     __shared__ XpShared S;
     load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -385,6 +405,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             S.ptm[t][1] = t1;
             S.pbon[t] = pack_bonus(d);
             S.pbk[t] = bk;
+            if (SH) S.proff[t] = base + t < n ? roff[base + t] : 0u;
         } else if (t < 2 * XP_PAR) {
             const int s = t - XP_PAR;
             S.phc[s] = hash_cards(S.plo[s], st_chi(S.phi[s]));
@@ -439,15 +460,36 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                 e[u] = i < nqb ? (uint32_t)S.qb[i] : (i < nq ? (uint32_t)S.qt[i - nqb] : 0xFFFFFFFFu);
                 key[u] = e[u] != 0xFFFFFFFFu ? child_key(e[u]) : 0;
             }
+            if (!SH) {   // the home slot's entry, loaded for all children together (SH: own children only, below)
 #pragma unroll
-            for (int u = 0; u < XP_U; u++)
-                if (e[u] != 0xFFFFFFFFu) ent[u] = load_entry(&tab[mix64(key[u]) & mask]);
+                for (int u = 0; u < XP_U; u++)
+                    if (e[u] != 0xFFFFFFFFu) ent[u] = load_entry(&tab[mix64(key[u]) & mask]);
+            }
 #pragma unroll
             for (int u = 0; u < XP_U; u++) {
                 if (e[u] == 0xFFFFFFFFu) continue;
                 const int s = (int)(e[u] & 31), dsc = (int)(e[u] >> 5);
-                const uint64_t tag = turn_tag | ((uint64_t)(base + s) << 8) | (uint64_t)dsc;
-                if (visit_claim_lm_pre(tab, mask, key[u], ent[u], tag, lost, err))
+                if (SH) {
+                    // record slot: the parent's first record + the child's ordinal (set bits below dsc in
+                    // its move space: buys 0..89, then the take patterns)
+                    uint64_t ms[3];
+                    move_space(S.pbl[s], S.pbh[s], S.ptm[s][0], S.ptm[s][1], ms);
+                    const int w0 = dsc >> 6;
+                    const uint64_t below = (1ull << (dsc & 63)) - 1;
+                    const uint32_t ord = (uint32_t)((w0 > 0 ? __popcll(ms[0]) : 0) + (w0 > 1 ? __popcll(ms[1]) : 0) +
+                                                    __popcll(ms[w0] & below));
+                    const uint32_t ri = S.proff[s] + ord;
+                    const uint32_t ow = owner_of(key[u], world);
+                    rdig[ri] = ow == me ? (uint8_t)0xFF : (uint8_t)ow;
+                    if (ow != me) {
+                        rkey[ri] = key[u];
+                        continue;
+                    }
+                }
+                const uint64_t tag = SH ? turn_tag | ((uint64_t)me << SH_Q_SHIFT) | ((uint64_t)(base + s) << 8) | (uint64_t)dsc
+                                        : turn_tag | ((uint64_t)(base + s) << 8) | (uint64_t)dsc;
+                if (SH) ent[u] = load_entry(&tab[mix64(key[u]) & mask]);
+                if (visit_claim_lm_pre<SH>(tab, mask, key[u], ent[u], tag, lost, err))
                     atomicOr(&S.cmask[s][dsc >> 6], 1ull << (dsc & 63));
             }
         }
@@ -760,6 +802,8 @@ struct Engine {
     double raw_ratio = 32.0;
     int n_grow = 0;
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
+    uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
+    std::vector<int64_t> srcb;            // sharded: first answer index of each source's records this turn
     int64_t pending_host = -1;
     double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
@@ -899,9 +943,9 @@ static void launch_front(Engine& E) {
     if (n > 0) {
         // a capped grid pulling groups of XP_PAR parents from a counter in rank order (a grid-stride
         // walk ran blocks a million ranks apart side by side: more displaced same-turn claims)
-        hipLaunchKernelGGL(k_expand, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables, cur.lo,
-                           cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1,
-                           E.d_small + 264);
+        hipLaunchKernelGGL(k_expand<false>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
+                           cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1,
+                           E.d_small + 264, 0u, 1u, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint8_t*)nullptr);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)

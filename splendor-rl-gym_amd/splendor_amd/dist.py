@@ -7,13 +7,14 @@ src/solver.py:452-456) stay global.  One step, per rank:
 
   turn sync one all_gather per turn of (slice size, first local position per pts): slice offsets and
             the goal check (src/solver.py:438-445)
-  expand    every successor of the local parents becomes a record (key, owner = mix64(key) top bits
-            mod world), grouped by owner in (parent, ordinal) order; one all_gather of the per-owner
-            counts sizes the exchange
+  expand    every successor of the local parents has an owner (mix64(key) top bits mod world); the
+            ones this rank owns are claimed in its shard of the global visited set during the
+            expansion, every other one becomes a record (key), grouped by owner in (parent, ordinal)
+            order; one all_gather of the per-owner counts sizes the exchange
   dedup     all_to_all of the keys to their owners; records arrive source rank by source rank, so
-            the record index at the owner is the global (parent rank, ordinal) order: the owner's
-            shard of the global visited set claims with tag = turn | record index and answers one
-            byte per record (first occurrence or not); all_to_all back
+            (source rank, record index) is the global (parent rank, ordinal) order: the owner claims
+            with tag = turn | source | index (its own children: turn | rank | parent | move) and
+            answers one bit per record (first occurrence or not); all_to_all back
   offsets   all_gather of per-rank unique counts -> this rank's next_queue offset k_off
   emit      survivors' states + scores; noise = accepted MT draw (consumed + k_off + k), from the
             sharded MT19937 stream (ShardNoise)
@@ -335,55 +336,47 @@ class DistSolve:
         src_tot = from_src.sum(axis=1)
         src_base = np.concatenate([[0], np.cumsum(src_tot)])        # global index base per source
         src_chunk = np.concatenate([np.zeros((c.world, 1), np.int64), np.cumsum(from_src, axis=1)], axis=1)
-        # this rank's own records never enter the exchange: they are claimed straight from send_key
-        # (no RCCL self-copy beside the claims; at world 1 there is no collective at all)
-        recv_x = from_src.copy()
-        recv_x[me, :] = 0
+        # this rank's own children were claimed in its expansion: it has no records for itself (and at
+        # world 1 there are no records and no collective at all)
+        assert int(from_src[me].sum()) == 0
         handles = []
         for j in range(C):
             pieces = [send_key[int(ostart[o] + ochunk[j, o]):int(ostart[o] + ochunk[j + 1, o])]
                       for o in range(c.world)]
-            self_piece = pieces[me]
             if c.world > 1:
-                pieces[me] = send_key[:0]
-                rkey, hd = c.alltoall_pieces(pieces, recv_x[:, j])
+                handles.append(c.alltoall_pieces(pieces, from_src[:, j]))
             else:
-                rkey, hd = send_key[:0], None
-            handles.append((self_piece, rkey, hd))
+                handles.append((send_key[:0], None))
         n_own = int(src_tot.sum())
-        b.owner_begin(n_own)
+        b.owner_begin(n_own, src_base[:-1])
         ret = b.answer_buffer(n_own)
-        for j, (self_piece, rkey, hd) in enumerate(handles):
-            if self_piece.numel():   # no wait: claims of any order settle to first occurrence
-                b.owner_claim(self_piece, [0], [int(src_base[me] + src_chunk[me, j])], ret)
+        for j, (rkey, hd) in enumerate(handles):   # claims of chunk j overlap the transfer of chunk j+1
             c.wait(hd)
             if rkey.numel():
-                starts = np.concatenate([[0], np.cumsum(recv_x[:, j])[:-1]])
+                starts = np.concatenate([[0], np.cumsum(from_src[:, j])[:-1]])
                 bases = src_base[:-1] + src_chunk[:, j]
                 b.owner_claim(rkey, starts, bases, ret)
         b.owner_finish(ret)
         self._mark(st, 'a2a_keys+claim')
-        # answers back to the sources; this rank's own answers are copied, not exchanged
+        # answers back to the sources, one bit per answer on the wire (8x less than the answer bytes)
         own_sz = ostart[1:] - ostart[:-1]
-        mine_ret = ret[int(src_base[me]):int(src_base[me + 1])]
-        if c.world > 1:   # one bit per answer on the wire (8x less than the answer bytes)
+        if c.world > 1:
             nb = lambda x: (int(x) + 7) // 8
-            sp = np.concatenate([[0], np.cumsum([nb(src_tot[q]) if q != me else 0 for q in range(c.world)])])
-            rp = np.concatenate([[0], np.cumsum([nb(own_sz[o]) if o != me else 0 for o in range(c.world)])])
+            sp = np.concatenate([[0], np.cumsum([nb(src_tot[q]) for q in range(c.world)])])
+            rp = np.concatenate([[0], np.cumsum([nb(own_sz[o]) for o in range(c.world)])])
             sbits = b.answer_buffer(int(sp[-1]))
             rbits = b.answer_buffer(int(rp[-1]))
             for q in range(c.world):
-                if q != me:
+                if src_tot[q]:
                     b.pack_bits(ret[int(src_base[q]):int(src_base[q + 1])], sbits[int(sp[q]):int(sp[q + 1])])
             c.alltoall_into([sbits[int(sp[q]):int(sp[q + 1])] for q in range(c.world)],
                             [rbits[int(rp[o]):int(rp[o + 1])] for o in range(c.world)])
             back = b.answer_buffer(int(ostart[-1]))
             for o in range(c.world):
-                if o != me:
+                if own_sz[o]:
                     b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o + 1])])
-            back[int(ostart[me]):int(ostart[me + 1])].copy_(mine_ret)
         else:
-            back = mine_ret
+            back = ret[:0]
         n_loc = b.apply(back)
         self._mark(st, 'dedup_exchange')
         all_n = c.allgather_int(n_loc)
@@ -527,7 +520,7 @@ class HipBackend:
         lib.sbd_goal_table.argtypes = [vp, vp]
         lib.sbd_expand.argtypes = [vp, i64, i32, i32, vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
-        lib.sbd_owner_begin.argtypes = [vp, i64]
+        lib.sbd_owner_begin.argtypes = [vp, i64, i32, vp]
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_owner_finish.argtypes = [vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
@@ -628,8 +621,9 @@ class HipBackend:
     def answer_buffer(self, n):
         return self._empty(max(int(n), 1), torch.uint8)[:int(n)]
 
-    def owner_begin(self, n_total):
-        self._chk(self.lib.sbd_owner_begin(self.h, int(n_total)), 'sbd_owner_begin')
+    def owner_begin(self, n_total, src_base):
+        sb = np.ascontiguousarray(np.asarray(src_base, dtype=np.int64))
+        self._chk(self.lib.sbd_owner_begin(self.h, int(n_total), len(sb), sb.ctypes.data), 'sbd_owner_begin')
 
     def owner_claim(self, rkey, starts, bases, ret):
         st = np.ascontiguousarray(starts, dtype=np.int64)

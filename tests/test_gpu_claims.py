@@ -18,9 +18,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _backend(log2):
+    """Owner rank 0 of a world of 2: every record comes from source rank 1 (a rank's own children never
+    become records, sbd_expand claims them itself)."""
     from splendor_amd.dist import HipBackend
     random.seed(0)
-    return HipBackend(rank=0, world=1, device_index=0, goal_pts=15, use_heuristic=False, heuristic=0,
+    return HipBackend(rank=0, world=2, device_index=0, goal_pts=15, use_heuristic=False, heuristic=0,
                       beam_width=1000, mt_state625=random.getstate()[1], visited_log2=log2)
 
 
@@ -46,11 +48,11 @@ def test_claims_first_occurrence_under_contention(order):
     try:
         dkeys = torch.from_numpy(keys.view(np.int64)).to(b.device)
         ret = b.answer_buffer(n)
-        b.owner_begin(n)
+        b.owner_begin(n, [0, 0])   # source 0 (this rank) sends nothing, source 1 all n records
         bounds = np.linspace(0, n, len(order) + 1).astype(np.int64)
         for c in order:   # chunks claimed out of index order: earlier records displace later holders
             a, e = int(bounds[c]), int(bounds[c + 1])
-            b.owner_claim(dkeys[a:e], [0], [a], ret)   # answers at the global record index
+            b.owner_claim(dkeys[a:e], [0, 0], [0, a], ret)   # source 1's records a..e, answers at index a..
         b.owner_finish(ret)
         torch.cuda.synchronize()
         got = ret.cpu().numpy()
