@@ -165,15 +165,17 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
  * between them are the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers
  * are caller-owned buffers on the engine's device.  The engine's work is ordered on its stream
  * (sbd_set_stream); calls that return host values wait for it. ---- */
-/* local first rank per pts of this rank's queue slice (0xFFFFFFFF = none) */
+/* local first rank per pts of this rank's queue slice (0xFFFFFFFF = none); after sbd_expand_launch it
+ * waits only for the table's copy, which was enqueued ahead of the expansion */
 int sbd_goal_table(sb_engine* e, uint32_t* first256);
-/* expand the local slice (global queue offset goff): the successors this rank owns (owner = fmix64(key)
- * >> 40 mod world) are claimed in its shard of the visited set; every other successor becomes a record
- * (key), stably partitioned by owner.  The records are cut into nchunk (<= 16)
- * exchange chunks of whole 4096-record tiles; chunk_owner_counts[nchunk][world] = records per chunk
- * and owner, *n_raw = successors generated */
-int sbd_expand(sb_engine* e, int64_t goff, int32_t world, int32_t nchunk, int64_t* chunk_owner_counts,
-               int64_t* n_raw);
+/* expand the local slice, in two calls.  sbd_expand_launch enqueues the expansion and returns without
+ * waiting (the caller launches it as soon as the slice exists, before its goal check): the successors
+ * this rank owns (owner = fmix64(key) >> 40 mod world) are claimed in its shard of the visited set, every
+ * other successor becomes a record (key).  sbd_expand_counts waits for it and stably partitions the
+ * records by owner, cut into nchunk (<= 16) exchange chunks of whole 4096-record tiles:
+ * chunk_owner_counts[nchunk][world] = records per chunk and owner, *n_raw = successors generated. */
+int sbd_expand_launch(sb_engine* e, int32_t world);
+int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts, int64_t* n_raw);
 /* the record keys grouped by owner, (parent, ordinal) order inside a group (d_tag unused: tags are
  * implicit in the order) */
 int sbd_pack(sb_engine* e, uint64_t* d_key, uint64_t* d_tag);
@@ -191,8 +193,11 @@ int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
  * unpack is the inverse (n answer bytes from ceil(n/8) packed bytes).  Both on the engine stream. */
 int sbd_pack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
 int sbd_unpack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
-/* apply the answers (in pack order); *n_unique_local = this rank's next_queue entries */
-int sbd_apply(sb_engine* e, const uint8_t* d_back, int64_t* n_unique_local);
+/* apply the answers (in pack order): this rank's next_queue entries as an int64 at n_unique_dev (device),
+ * without waiting (the caller all-gathers it on the engine stream); sbd_apply_finish(that value) then
+ * checks the step's error word and updates the host state. */
+int sbd_apply(sb_engine* e, const uint8_t* d_back, void* n_unique_dev);
+int sbd_apply_finish(sb_engine* e, int64_t n_unique_local);
 /* states + scores of the local survivors; next_queue positions k_off.., n_total draws consumed */
 int sbd_emit(sb_engine* e, uint64_t k_off, uint64_t n_total, int64_t goff);
 /* Sharded noise stream (heuristic, sharded mode): rank r generates MT19937 chunks c = r (mod world),
@@ -234,12 +239,13 @@ int sbd_sel_compact(sb_engine* e);
 int sbd_sel_eq(sb_engine* e, void* eq_dev);
 /* kept = key > T or (key == T and global tie index < its position) [if has_top; T = position 0's key,
  * eq_all_dev = every rank's tie count]; destination range = #{j : key < split_j} (splits = the next
- * nsplit positions' keys); dest_counts[world] */
+ * nsplit positions' keys); dest_counts_dev = int64[world] records per destination, on the device (no wait) */
 int sbd_partition(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t nsplit, int32_t world,
-                  int64_t* dest_counts);
-int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, int64_t* dest_counts);
+                  void* dest_counts_dev);
+int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, void* dest_counts_dev);
 /* kept records grouped by destination, next_queue order inside a group: 4 x u64 per record
- * (state lo, state hi, global parent rank, score key), one all_to_all buffer */
+ * (state lo, state hi, global parent rank, score key), one all_to_all buffer of at least the kept count
+ * (the local next_queue size always suffices, so it can be enqueued before the counts reach the host) */
 int sbd_pack_kept(sb_engine* e, uint64_t* d_rec);
 /* the new slice: n received 4-word records (global next_queue order), stable-sorted by score if heur */
 int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);

@@ -469,7 +469,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
             for (int u = 0; u < XP_U; u++) {
                 if (e[u] == 0xFFFFFFFFu) continue;
                 const int s = (int)(e[u] & 31), dsc = (int)(e[u] >> 5);
-                if (SH) {
+                if (SH && world > 1) {
                     // record slot: the parent's first record + the child's ordinal (set bits below dsc in
                     // its move space: buys 0..89, then the take patterns)
                     uint64_t ms[3];
@@ -802,6 +802,10 @@ struct Engine {
     double raw_ratio = 32.0;
     int n_grow = 0;
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
+    bool records = true;                  // sharded: this turn made records for other owners (world > 1)
+    bool apply_pending = false;           // sharded: sbd_apply done, sbd_apply_finish not yet
+    bool expand_pending = false;          // sharded: sbd_expand_launch done, sbd_expand_counts not yet
+    int expand_world = 1;
     uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
     std::vector<int64_t> srcb;            // sharded: first answer index of each source's records this turn
     int64_t pending_host = -1;
@@ -874,9 +878,13 @@ static void preallocate_dist(Engine& E) {
     E.surv.ensure(wl * 3);
     E.cnt.ensure(wl);
     E.off.ensure(wl);
-    E.cand_key.ensure(nr);
-    E.cand_pos.ensure(nr);
-    E.digit.ensure(nr);
+    E.cand.ensure(wl * 3);
+    E.lost.ensure(wl * 3);
+    if (E.cfg.world_size > 1) {   // record buffers for the worst case: sbd_expand_launch needs no host count
+        E.cand_key.ensure(wl * MAX_CHILDREN);
+        E.cand_pos.ensure(wl * MAX_CHILDREN);
+        E.digit.ensure(wl * MAX_CHILDREN);
+    }
     E.own_lost.ensure(nr / 64 + 1);
     E.nlo.ensure(nu);
     E.nhi.ensure(nu);

@@ -52,6 +52,9 @@ class Comm:
         self.device = device
         self.backend = dist.get_backend()
         self.cpu_coll = self.backend == 'gloo'
+        # host-side metadata (the turn sync: slice sizes + goal tables) goes over a gloo group: it runs
+        # while the expansion occupies every CU, which a device collective would have to wait for
+        self.meta = dist.new_group(backend='gloo') if self.world > 1 else None
 
     def _to(self, t):
         return t.cpu() if self.cpu_coll else t
@@ -68,6 +71,8 @@ class Comm:
         """Every rank's equal-shape tensor, concatenated rank-major in one flat tensor: one collective
         (all_gather_into_tensor), so the host reads it back with one copy instead of one per rank."""
         s = self._to(t).reshape(-1)
+        if self.world == 1:
+            return s
         out = torch.empty(self.world * s.numel(), dtype=s.dtype, device=s.device)
         dist.all_gather_into_tensor(out, s)
         return out
@@ -75,6 +80,21 @@ class Comm:
     def allgather_int(self, v: int) -> np.ndarray:
         t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
         return self._gather_flat(t).cpu().numpy().astype(np.int64)
+
+    def gather_dev(self, t: torch.Tensor) -> np.ndarray:
+        """Every rank's equal-shape device tensor, concatenated rank-major, on the host (one wait)."""
+        return self._gather_flat(t).cpu().numpy()
+
+    def alltoall_counts_dev(self, counts: torch.Tensor) -> tuple[np.ndarray, np.ndarray]:
+        """(send counts, receive counts) on the host from a device tensor of send counts: one wait."""
+        if self.world == 1:
+            c = counts.cpu().numpy()
+            return c, c
+        send = self._to(counts)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send)
+        both = torch.cat([send, recv]).cpu().numpy()
+        return both[:self.world], both[self.world:]
 
     def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
         send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
@@ -121,6 +141,8 @@ class Comm:
 
     def allreduce_tensor(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
         """In-place reduction over ranks of a tensor on this rank's device (no host wait with RCCL)."""
+        if self.world == 1:
+            return
         if self.cpu_coll:
             x = t.cpu()
             dist.all_reduce(x, op=op)
@@ -128,9 +150,17 @@ class Comm:
         else:
             dist.all_reduce(t, op=op)
 
-    def allgather_array(self, arr: np.ndarray) -> np.ndarray:
-        """(world, len) int64 array of every rank's equal-length int vector."""
+    def allgather_array(self, arr: np.ndarray, host: bool = False) -> np.ndarray:
+        """(world, len) int64 array of every rank's equal-length int vector (host: over the gloo metadata
+        group, no device work)."""
         a = np.ascontiguousarray(arr, dtype=np.int64)
+        if host:
+            if self.world == 1:
+                return a.reshape(1, len(a))
+            t = torch.from_numpy(a)
+            out = [torch.empty_like(t) for _ in range(self.world)]
+            dist.all_gather(out, t, group=self.meta)
+            return torch.stack(out).numpy()
         t = torch.from_numpy(a).to(self.device)
         return self._gather_flat(t).cpu().numpy().reshape(self.world, len(a))
 
@@ -253,6 +283,7 @@ class DistSolve:
         self.max_pts = 0
         self.winner = None                      # (turn, global rank)
         self.counts = []                        # per turn: per-rank slice sizes
+        self.b.expand_launch(self.c.world)      # runs while the host does the turn sync / goal check
         self._turn_sync()
         self.noise = ShardNoise(backend, comm) if use_heuristic else None
         self.consumed = 0                       # accepted draws used so far (global)
@@ -268,7 +299,7 @@ class DistSolve:
         """Once per turn, one all_gather: every rank's slice size and its first local position per
         pts value, giving the slice offsets and the global first position per pts."""
         gt = self.b.goal_table().astype(np.int64)
-        M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt]))
+        M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt]), host=True)
         cnt = M[:, 0].copy()
         offs = np.concatenate([[0], np.cumsum(cnt)[:-1]])
         first = M[:, 1:]
@@ -318,10 +349,10 @@ class DistSolve:
             st.update(done=True, winner_rank=win)
             return st
         off = self.offset()
-        # local expansion + local filter; candidate records grouped by owner
-        # exchange chunks: claims of chunk j overlap the transfer of chunk j+1
+        # the expansion (launched when this slice arrived) claimed the own children; the records for the
+        # other owners are partitioned by owner.  Exchange chunks: claims of chunk j overlap chunk j+1's transfer
         C = self.nchunk if st['n_parents'] * 24 >= self.chunk_min else 1
-        cc, n_raw = b.expand(off, self.turn, c.world, C)            # (C, world) records per chunk, owner
+        cc, n_raw = b.expand_counts(C)                              # (C, world) records per chunk, owner
         M = c.allgather_array(np.concatenate([cc.ravel(), [n_raw]]))
         st['n_raw'] = int(M[:, -1].sum())
         Mc = M[:, :-1].reshape(c.world, C, c.world)                 # [source][chunk][owner]
@@ -377,9 +408,9 @@ class DistSolve:
                     b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o + 1])])
         else:
             back = ret[:0]
-        n_loc = b.apply(back)
+        all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
+        b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
-        all_n = c.allgather_int(n_loc)
         k_off = int(all_n[:c.rank].sum())
         N = int(all_n.sum())
         st['n_unique'] = N
@@ -406,14 +437,14 @@ class DistSolve:
                 if has_top:
                     eq_all = c.allgather_tensor(b.sel_eq()).reshape(-1)
             self._mark(st, 'sel_eq')
-            dest_counts = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
+            dest_dev = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
         else:
-            dest_counts = b.partition_bfs(k_off, N, G)
+            dest_dev = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
-        rec = b.pack_kept()
+        rec = b.pack_kept(all_n[c.rank])   # enqueued ahead of the counts' round trip
+        dest_counts, recv = c.alltoall_counts_dev(dest_dev)
         self._mark(st, 'pack_kept')
         if c.world > 1:   # records arrive source rank by source rank; this rank's own are copied
-            recv = c.alltoall_counts(dest_counts)
             me = c.rank
             so = np.concatenate([[0], np.cumsum(dest_counts)]).astype(np.int64)
             ro = np.concatenate([[0], np.cumsum(recv)]).astype(np.int64)
@@ -423,9 +454,10 @@ class DistSolve:
             c.alltoall_into(pieces, outs)
             rrec[int(ro[me]):int(ro[me + 1])].copy_(rec[int(so[me]):int(so[me + 1])])
         else:
-            rrec = rec
+            rrec = rec[:int(dest_counts.sum())]
         self._mark(st, 'a2a_kept')
         b.receive(rrec, self.heur)
+        b.expand_launch(c.world)   # the next turn's expansion overlaps its goal check
         self._turn_sync()
         self._mark(st, 'rebalance')
         self.turn += 1
@@ -518,14 +550,16 @@ class HipBackend:
         vp, i64, u64, i32 = C.c_void_p, C.c_int64, C.c_uint64, C.c_int32
         p64 = C.POINTER(C.c_int64)
         lib.sbd_goal_table.argtypes = [vp, vp]
-        lib.sbd_expand.argtypes = [vp, i64, i32, i32, vp, p64]
+        lib.sbd_expand_launch.argtypes = [vp, i32]
+        lib.sbd_expand_counts.argtypes = [vp, i32, vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
         lib.sbd_owner_begin.argtypes = [vp, i64, i32, vp]
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_owner_finish.argtypes = [vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_unpack_bits.argtypes = [vp, vp, i64, vp]
-        lib.sbd_apply.argtypes = [vp, vp, p64]
+        lib.sbd_apply.argtypes = [vp, vp, vp]
+        lib.sbd_apply_finish.argtypes = [vp, i64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_key_range.argtypes = [vp, vp]
         lib.sbd_sel_begin.argtypes = [vp, i32, vp, vp]
@@ -600,14 +634,20 @@ class HipBackend:
         return self.L.visited_capacity(self.h)
 
     # ---------------------------------------------------------------- step primitives
-    def expand(self, off, turn, world, nchunk=1):
+    def expand_launch(self, world):
+        """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait."""
+        self.world_x = int(world)
+        self._chk(self.lib.sbd_expand_launch(self.h, int(world)), 'sbd_expand_launch')
+
+    def expand_counts(self, nchunk=1):
+        """Wait for the expansion; (nchunk, world) records per exchange chunk and owner, raw total."""
         C = self.C
-        counts = np.zeros(nchunk * world, np.int64)
+        counts = np.zeros(nchunk * self.world_x, np.int64)
         nraw = C.c_int64()
-        self._chk(self.lib.sbd_expand(self.h, int(off), int(world), int(nchunk), counts.ctypes.data, C.byref(nraw)),
-                  'sbd_expand')
-        self.owner_counts = counts.reshape(nchunk, world).sum(axis=0)
-        return counts.reshape(nchunk, world), nraw.value
+        self._chk(self.lib.sbd_expand_counts(self.h, int(nchunk), counts.ctypes.data, C.byref(nraw)),
+                  'sbd_expand_counts')
+        self.owner_counts = counts.reshape(nchunk, self.world_x).sum(axis=0)
+        return counts.reshape(nchunk, self.world_x), nraw.value
 
     def _empty(self, n, dtype=torch.int64):
         return torch.empty(int(n), dtype=dtype, device=self.device)
@@ -644,9 +684,13 @@ class HipBackend:
             self._chk(self.lib.sbd_unpack_bits(self.h, src.data_ptr(), dst.numel(), dst.data_ptr()), 'sbd_unpack_bits')
 
     def apply(self, back):
-        n = self.C.c_int64()
-        self._chk(self.lib.sbd_apply(self.h, back.data_ptr(), self.C.byref(n)), 'sbd_apply')
-        return n.value
+        """Survivor masks from the answers; this rank's unique count as a device int64 (no wait)."""
+        n = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_apply(self.h, back.data_ptr(), n.data_ptr()), 'sbd_apply')
+        return n
+
+    def apply_finish(self, n_loc):
+        self._chk(self.lib.sbd_apply_finish(self.h, int(n_loc)), 'sbd_apply_finish')
 
     def noise_info(self):
         out = np.zeros(8, np.uint64)
@@ -705,23 +749,23 @@ class HipBackend:
         return self.sel_eqbuf
 
     def partition(self, has_top, eq_all, rank, nsplit, G):
-        counts = np.zeros(G, np.int64)
+        """Kept records' destinations; per-destination counts as a device int64 tensor (no wait)."""
+        counts = torch.zeros(G, dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_partition(self.h, int(bool(has_top)), eq_all.data_ptr() if eq_all is not None else None,
-                                         int(rank), int(nsplit), int(G), counts.ctypes.data), 'sbd_partition')
-        self.dest_counts = counts
+                                         int(rank), int(nsplit), int(G), counts.data_ptr()), 'sbd_partition')
         return counts
 
     def partition_bfs(self, k_off, N, G):
-        counts = np.zeros(G, np.int64)
-        self._chk(self.lib.sbd_partition_bfs(self.h, int(k_off), int(N), int(G), counts.ctypes.data),
+        counts = torch.zeros(G, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_partition_bfs(self.h, int(k_off), int(N), int(G), counts.data_ptr()),
                   'sbd_partition_bfs')
-        self.dest_counts = counts
         return counts
 
-    def pack_kept(self):
-        n = int(self.dest_counts.sum())
-        rec = torch.empty((n, 4), dtype=torch.int64, device=self.device)
-        self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n else None), 'sbd_pack_kept')
+    def pack_kept(self, n_rows):
+        """Kept records grouped by destination into a buffer of n_rows (>= the kept count: the local
+        next_queue size), enqueued before the counts reach the host."""
+        rec = torch.empty((max(int(n_rows), 1), 4), dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None), 'sbd_pack_kept')
         return rec
 
     def receive(self, rec, heur):
