@@ -73,18 +73,20 @@ def expand_bytes(n_parents, n_raw, n_cand_new):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary (profiles/)."""
+    """(HBM bytes per launch, trace average ns, L2 hit rate, source) of `kernel` (or its template instance
+    used by this path, e.g. k_expand<false>) from the newest committed rocprofv3 PMC summary (profiles/)."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_profile_summary.json')))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            v = d['pmc'][kernel]['hbm_bytes_per_launch']
-            t = d['timed'][kernel]['avg_ns']
-            return v, t, os.path.relpath(f, REPO)
-        except (KeyError, ValueError, OSError):
+            name = next(k for k in d['pmc'] if k == kernel or k == kernel + '<false>')
+            v = d['pmc'][name]['hbm_bytes_per_launch']
+            t = d['timed'][name]['avg_ns']
+            return v, t, d['pmc'][name].get('tcc_hit_rate'), os.path.relpath(f, REPO)
+        except (KeyError, ValueError, OSError, StopIteration):
             continue
-    return None, None, None
+    return None, None, None, None
 
 
 def step_bytes(n_parents, n_raw, n_unique, n_kept):
@@ -359,10 +361,12 @@ def main():
             'touches_per_launch': int(touches), 'achieved_G_per_s': round(touches / (ms_dom * 1e-3) / 1e9, 2),
             'peak_G_per_s': RANDOM_LOAD_PEAK_G, 'frac': round(touches / (ms_dom * 1e-3) / 1e9 / RANDOM_LOAD_PEAK_G, 3),
             'peak_source': 'profiles/micro/r1_randaccess.txt (load16, 32 GiB table)'}
-    tr, tns, src = pmc_traffic(dom.replace('ms_', 'k_'))
+    tr, tns, hit, src = pmc_traffic(dom.replace('ms_', 'k_'))
     if tr is not None:
         out['roofline']['traffic'] = int(tr)
         out['roofline']['traffic_GBps'] = round(tr / (tns * 1e-9) / 1e9, 1)
+        if hit is not None:
+            out['roofline']['l2_hit_rate'] = round(hit, 4)
         out['roofline']['traffic_source'] = f'{src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; ' \
                                             f'hbm = (2*FETCH + WRITE) KiB, gfx950 correction)'
     if not args.no_cpu_baseline:

@@ -18,6 +18,23 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+REPO = os.path.dirname(os.path.abspath(__file__))
+
+
+def sharded_pmc():
+    """k_expand<true> (the sharded step's dominant kernel: own claims + records) from the newest committed
+    sharded PMC summary (profiles/r*_profile_sharded_summary.json), or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_profile_sharded_summary.json')), reverse=True):
+        try:
+            d = json.load(open(f))
+            v = d['pmc']['k_expand<true>']
+            return {'kernel': 'k_expand<true>', 'hbm_bytes_per_launch': int(v['hbm_bytes_per_launch']),
+                    'source': os.path.relpath(f, REPO) + ' (world 1, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)'}
+        except (KeyError, ValueError, OSError):
+            continue
+    return None
+
 
 def main(args):
     # RCCL prints its version banner on stdout at init: keep stdout for the one JSON line
@@ -87,6 +104,11 @@ def main(args):
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
             'cpu_baseline': None,
         }
+        sh = sharded_pmc()
+        if sh:   # the dominant kernel's HBM bytes per launch, profiled on the sharded path at world 1
+            out['roofline']['traffic'] = sh['hbm_bytes_per_launch']
+            out['roofline']['traffic_kernel'] = sh['kernel']
+            out['roofline']['traffic_source'] = sh['source']
         if not args.no_cpu_baseline:   # after the timed region; the other ranks wait at the barrier below
             out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, min(args.cpu_budget_s, 20.0))
         sys.stdout.flush()

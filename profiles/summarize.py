@@ -17,7 +17,7 @@ from collections import defaultdict
 
 # kernels launched once per step on the saturated path (k_expand: the last launches include the
 # pipelined expansion of the turn after the last timed one — one per step either way)
-PER_STEP = ['k_expand', 'k_count_lm', 'k_emit_w<1, false>', 'k_tk_count', 'k_tk_write', 'k_os_hist', 'k_os_pass',
+PER_STEP = ['k_expand<false>', 'k_expand<true>', 'k_count_lm', 'k_emit_w<1, false>', 'k_tk_count', 'k_tk_write', 'k_os_hist', 'k_os_pass',
             'k_gather_d', 'k_copy_idx']
 
 
@@ -47,7 +47,7 @@ def main():
         """Dispatches of the timed turns: the expansion of the first timed turn is launched (pipelined)
         inside the step before it, the expansion after the last timed turn inside the last timed step;
         the timed turns' kernels lie between those two expansion starts."""
-        ex = [r for r in recs if r[0] == 'k_expand']
+        ex = [r for r in recs if r[0].startswith('k_expand')]
         t0, t1 = ex[-a.steps - 1][1], ex[-1][1]
         return [r for r in recs if t0 <= r[1] < t1]
 
@@ -67,7 +67,8 @@ def main():
             d = win[k]
             timed[k] = {'launches': len(d), 'avg_ns': sum(d) / len(d), 'per_step_ns': sum(d) / a.steps}
     pmc = {}
-    for kind, fn in (('FETCH_SIZE', 'pmc_fetch'), ('WRITE_SIZE', 'pmc_write')):
+    for kind, fn in (('FETCH_SIZE', 'pmc_fetch'), ('WRITE_SIZE', 'pmc_write'), ('TCC_HIT_sum', 'pmc_tcc'),
+                     ('TCC_MISS_sum', 'pmc_tcc')):
         p = os.path.join(a.dir, fn, 'run_counter_collection.csv')
         if not os.path.exists(p):
             continue
@@ -75,10 +76,14 @@ def main():
         for r in timed_window(load(p, kind)):
             vals[r[0]].append(r[3])
         for k, v in vals.items():
-            pmc.setdefault(k, {})[kind + '_KiB_timed_avg'] = sum(v) / len(v)
+            unit = '_KiB_timed_avg' if kind.endswith('SIZE') else '_timed_avg'
+            pmc.setdefault(k, {})[kind + unit] = sum(v) / len(v)
     for k, v in pmc.items():
         if 'FETCH_SIZE_KiB_timed_avg' in v and 'WRITE_SIZE_KiB_timed_avg' in v:
             v['hbm_bytes_per_launch'] = (2 * v['FETCH_SIZE_KiB_timed_avg'] + v['WRITE_SIZE_KiB_timed_avg']) * 1024
+        if 'TCC_HIT_sum_timed_avg' in v and 'TCC_MISS_sum_timed_avg' in v:
+            h, m = v['TCC_HIT_sum_timed_avg'], v['TCC_MISS_sum_timed_avg']
+            v['tcc_hit_rate'] = h / (h + m) if h + m else None
     bench = None
     bp = os.path.join(a.dir, 'bench_trace.json')
     if os.path.exists(bp):
