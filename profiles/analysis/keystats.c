@@ -74,6 +74,22 @@ int main(int argc, char** argv) {
     printf("select bins (key>>47) spanned %llu  largest kept bin %lld  kept above T's bin %lld  all keys in T's bin %lld\n",
            (unsigned long long)(bM - bT + 1), (long long)big, (long long)above_bin,
            (long long)({ int64_t c = 0; for (int64_t i = 0; i < m; i++) c += (keys[i] >> 47) == bT; c; }));
+    // the sort's prefix: (key - T) >> sh; pairs of adjacent different keys sharing a prefix = fix-up work
+    for (int sh = 29; sh >= 5; sh -= 4) {
+        int64_t pairs = 0, runs = 0, runel = 0;
+        for (int64_t i = 1; i < k; i++) {
+            const int same = ((keys[i] - T) >> sh) == ((keys[i - 1] - T) >> sh);
+            if (same && keys[i] != keys[i - 1]) pairs++;
+        }
+        for (int64_t i = 0; i < k;) {   // runs of equal prefix holding > 1 distinct key
+            int64_t j = i + 1, diff = 0;
+            while (j < k && ((keys[j] - T) >> sh) == ((keys[i] - T) >> sh)) { diff |= keys[j] != keys[j - 1]; j++; }
+            if (diff) { runs++; runel += j - i; }
+            i = j;
+        }
+        printf("prefix (key-T)>>%d (%d bits): %lld flagged pairs, %lld runs to fix, %lld elements in them\n", sh,
+               64 - __builtin_clzll(mx - T) - sh, (long long)pairs, (long long)runs, (long long)runel);
+    }
     for (int sh = 40; sh >= 24; sh -= 8) {
         int64_t groups = 1, gbig = 0, gcur = 0;
         for (int64_t i = 1; i <= k; i++) {

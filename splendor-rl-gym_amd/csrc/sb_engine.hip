@@ -858,6 +858,7 @@ static void check_err_word(Engine& E) {
     if (e & 4u) throw HipError{hipErrorLaunchFailure, "top-k sort look-back wait exceeded its bound"};
     if (e & 8u) throw HipError{hipErrorLaunchFailure, "sharded answers do not match the parents' move counts"};
     if (e & 16u) throw HipError{hipErrorInvalidValue, "heuristic returned NaN: no stable sort order exists"};
+    if (e & 32u) throw HipError{hipErrorLaunchFailure, "top-k sort fix-up: more distinct keys in one prefix run than it holds"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {

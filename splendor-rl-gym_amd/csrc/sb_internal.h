@@ -100,6 +100,9 @@ struct TopkScratch {
     DBuf<uint64_t> os;              // LSD sort: digit histograms, tickets, look-back granules
     DBuf<uint32_t> tile_a, tile_b;  // partition counts
     DBuf<uint64_t> small;           // select state + histogram
+    DBuf<uint32_t> fx_list;         // sort fix-up: flagged positions
+    DBuf<uint32_t> fx_mark;         // sort fix-up: run claims (epoch stamps)
+    uint32_t fx_epoch = 0;
     void release();
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.

@@ -12,10 +12,12 @@
 //      (first in index order) are kept; a final partition appends the candidates above T, then those
 //      ties.  The three output groups have disjoint key sets, so a stable sort of the concatenation
 //      orders ties by index exactly as sorted() does;
-//   5. a stable LSD radix sort (8-bit digits) on ~key orders the kept set, one kernel per digit with
-//      decoupled look-back; digits above the highest bit that differs inside [lowest kept key, max]
-//      are constant and skipped on the device.  (Measured on 4M keys, profiles/sortbench.py: 47 us
-//      per pass, 35 of them without the look-back wait; 90 us for the histograms of all digits.)
+//   5. a stable LSD radix sort (8-bit digits) orders the kept set by the top 40 of the bits that vary
+//      inside [lowest kept key, max] (at most 5 passes, one kernel per digit with decoupled look-back;
+//      about 50 us per pass on 4M keys).  Keys are f64 score images: on C3 the kept 4M hold ~115k
+//      distinct values over 53 varying bits, and no two of them share a 40-bit prefix (814 pairs do at
+//      32 bits, 59 at 36: profiles/analysis/keystats.c, turn 12); 6. an exact fix-up re-orders any run
+//      of equal prefixes that still holds different keys, stably by the full key.
 #include <algorithm>
 
 #include "sb_block.h"
@@ -29,6 +31,12 @@ constexpr int TK_TILE = TK_NT * TK_IPT;   // 4096
 constexpr int SEL_D = 11;                 // select digit bits
 constexpr int SEL_BINS = 1 << SEL_D;
 constexpr int SEL_PASSES_C = 6;           // candidate passes: ceil(64 / 11) upper bound
+#ifndef SB_SORT_PREFIX_BITS
+#define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
+#endif
+constexpr int OS_PREFIX_BITS = SB_SORT_PREFIX_BITS;
+constexpr int OS_MAX_PASSES = (OS_PREFIX_BITS + 7) / 8;
+
 
 // device state (u64 words)
 enum : int {
@@ -42,8 +50,11 @@ enum : int {
     ST_TOPK,    // sort: bits [0, TOPK) vary among the kept keys
     ST_FBASE,   // fused first pass: histogram bin b counts keys with key >> 47 == FBASE + b (edges clamped)
     ST_FALLBACK,  // fused first pass unusable (threshold in a clamped bin): run the generic first pass
-    ST_SLO,     // sort: lowest possible kept key; digits are taken from key - SLO
-    ST_HIST = 16,
+    ST_SLO,     // sort: lowest possible kept key; digits are taken from (key - SLO) >> SH32
+    ST_SH32,    // sort: low bits below the sorted 40-bit prefix
+    ST_FXN,     // fix-up: flagged positions (prefix equal to the predecessor's, key not)
+    ST_FXI,     // fix-up: work counter over the flagged positions
+    ST_HIST = 20,
     ST_WORDS = ST_HIST + SEL_BINS
 };
 
@@ -349,8 +360,12 @@ __global__ void k_tk_sortsetup(uint64_t* st, int selected) {
     uint64_t lo = st[ST_MIN];
     if (selected) lo = st[ST_SH] >= 64 ? 0ull : (st[ST_PREFIX] << st[ST_SH]);
     const uint64_t x = st[ST_MAX] - lo;
+    const uint64_t topk = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
     st[ST_SLO] = lo;
-    st[ST_TOPK] = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
+    st[ST_TOPK] = topk;
+    st[ST_SH32] = topk > OS_PREFIX_BITS ? topk - OS_PREFIX_BITS : 0;   // the sort orders the top varying bits
+    st[ST_FXN] = 0;
+    st[ST_FXI] = 0;
 }
 
 // ---- stable LSD radix sort of the kept set, one kernel per 8-bit digit (decoupled look-back)
@@ -386,7 +401,8 @@ __device__ __forceinline__ uint64_t os_poll(const uint64_t* p) {
     return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] + 7) / 8); }
+__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] - st[ST_SH32] + 7) / 8); }
+__device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64_t sh) { return (k - slo) >> sh; }
 
 // histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
 // cluster); 16 loads in flight per thread
@@ -401,7 +417,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
                                                    const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     __shared__ uint32_t hh[OSH_NH][8][256];
     const int P = sort_passes(st);
-    const uint64_t slo = st[ST_SLO];
+    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
     for (int i = threadIdx.x; i < OSH_NH * 8 * 256; i += OS_NT) (&hh[0][0][0])[i] = 0;
     __syncthreads();
     uint32_t (*h)[256] = hh[SB_OSH_WH ? (threadIdx.x >> 6) : 0];
@@ -410,7 +426,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
     for (int64_t i0 = (int64_t)blockIdx.x * OS_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
         uint64_t kk[OS_IPT];
 #pragma unroll
-        for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~(keys[i0 + r * stride] - slo) : 0ull;
+        for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~sort_prefix(keys[i0 + r * stride], slo, sh) : 0ull;
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const bool valid = i0 + r * stride < n;
@@ -460,7 +476,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     const int64_t tile = s_tile;
     const int64_t base = tile * OS_TILE;
     const int shift = 8 * p;
-    const uint64_t slo = st[ST_SLO];
+    const uint64_t slo = st[ST_SLO], psh = st[ST_SH32];
     const uint64_t lt = lanemask_lt();
     uint64_t kk[OS_IPT];
     uint32_t vv[OS_IPT];
@@ -475,7 +491,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     for (int r = 0; r < OS_IPT; r++) {
         const int64_t i = base + (int64_t)r * OS_NT + t;
         const bool valid = i < n;
-        const uint32_t d = (uint32_t)(((~(kk[r] - slo)) >> shift) & 255);
+        const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & 255);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -549,6 +565,177 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     }
 }
 
+// ---- exact fix-up of the 40-bit-prefix sort.  Sorted output = (prefix desc, input order); the required
+// order is (key desc, input order) — input order is next_queue order among equal keys (the select writes
+// each key set in index order).  k_fx_mark lists the positions whose prefix equals the predecessor's but
+// whose key does not; k_fx_fix claims each such position's run of equal prefixes once (epoch-stamped run
+// marks), counts its distinct keys (an LDS set; a run holds a handful), and places every element at
+// start(its key, in descending key order) + its rank among equal keys in run order — one wave, 64
+// elements per round, so the placement is stable — through the other ping-pong buffer.
+constexpr int FX_NT = 256;
+constexpr int FX_SET = 1024;   // distinct keys per run (more sets error bit 32: never expected)
+constexpr int FX_LIST = 256;   // distinct keys placed by the compact start computation
+
+__global__ __launch_bounds__(256) void k_fx_mark(const uint64_t* k0, const uint64_t* k1, int64_t m, uint64_t* st,
+                                                 uint32_t* __restrict__ list) {
+    const uint64_t* kf = (sort_passes(st) & 1) ? k1 : k0;
+    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
+    if (sh == 0) return;   // the prefix is the whole key: nothing to fix
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = kf[i - 1], b = kf[i];
+        if (a != b && sort_prefix(a, slo, sh) == sort_prefix(b, slo, sh)) {
+            const uint64_t j = atomicAdd((unsigned long long*)&st[ST_FXN], 1ull);
+            list[j] = (uint32_t)i;
+        }
+    }
+}
+
+__global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t m,
+                                                  uint64_t* st, const uint32_t* __restrict__ list,
+                                                  uint32_t* __restrict__ runmark, uint32_t epoch, uint32_t* err) {
+    const int P = sort_passes(st);
+    uint64_t* kf = (P & 1) ? k1 : k0;
+    uint32_t* vf = (P & 1) ? v1 : v0;
+    uint64_t* ka = (P & 1) ? k0 : k1;   // the other buffer: scratch for the run
+    uint32_t* va = (P & 1) ? v0 : v1;
+    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32], nflag = st[ST_FXN];
+    __shared__ uint64_t skey[FX_SET];
+    __shared__ uint32_t scnt[FX_SET], sstart[FX_SET];
+    __shared__ uint64_t lkey[FX_LIST];
+    __shared__ uint32_t lslot[FX_LIST];
+    __shared__ uint64_t sa, sb, sj;
+    __shared__ uint32_t go, nd;
+    const int t = threadIdx.x;
+    for (;;) {
+        if (t == 0) sj = atomicAdd((unsigned long long*)&st[ST_FXI], 1ull);
+        __syncthreads();
+        const uint64_t j = sj;
+        if (j >= nflag) return;
+        const int64_t i = list[j];
+        const uint64_t pre = sort_prefix(kf[i], slo, sh);
+        // the run [a, b) of equal prefixes around i: the block walks out 256 positions at a time
+        if (t == 0) {
+            sa = (uint64_t)i;
+            sb = (uint64_t)i + 1;
+        }
+        __syncthreads();
+        for (int64_t base = i - 1;; base -= FX_NT) {
+            const int64_t q = base - t;
+            const bool same = q >= 0 && sort_prefix(kf[q], slo, sh) == pre;
+            if (same) atomicMin((unsigned long long*)&sa, (unsigned long long)q);
+            const int any_out = __syncthreads_or(!same);
+            if (any_out) break;
+        }
+        for (int64_t base = i + 1;; base += FX_NT) {
+            const int64_t q = base + t;
+            const bool same = q < m && sort_prefix(kf[q], slo, sh) == pre;
+            if (same) atomicMax((unsigned long long*)&sb, (unsigned long long)(q + 1));
+            const int any_out = __syncthreads_or(!same);
+            if (any_out) break;
+        }
+        // claim the run once per sort call (several flagged positions can share it)
+        if (t == 0) {
+            uint32_t old = runmark[sa];
+            go = 0;
+            while (old != epoch) {
+                const uint32_t got = atomicCAS(&runmark[sa], old, epoch);
+                if (got == old) {
+                    go = 1;
+                    break;
+                }
+                old = got;
+            }
+            nd = 0;
+        }
+        __syncthreads();
+        if (!go) continue;
+        const int64_t a = (int64_t)sa, b = (int64_t)sb;
+        const uint64_t none = kf[a] ^ (1ull << 63);   // no key of the run: they lie within 2^32 of each other
+        for (int x = t; x < FX_SET; x += FX_NT) {
+            skey[x] = none;
+            scnt[x] = 0;
+        }
+        __syncthreads();
+        // distinct keys of the run and their counts (an LDS set, linear probing on the key)
+        for (int64_t q = a + t; q < b; q += FX_NT) {
+            const uint64_t k = kf[q];
+            uint32_t h = (uint32_t)(k ^ (k >> 29)) & (FX_SET - 1);
+            for (int probe = 0;; probe++) {
+                if (probe == FX_SET) {
+                    if (err) atomicOr(err, 32u);
+                    break;
+                }
+                const unsigned long long prev = atomicCAS((unsigned long long*)&skey[h], (unsigned long long)none,
+                                                          (unsigned long long)k);
+                if (prev == none || prev == k) {
+                    atomicAdd(&scnt[h], 1u);
+                    break;
+                }
+                h = (h + 1) & (FX_SET - 1);
+            }
+        }
+        __syncthreads();
+        // start of each distinct key in the run: elements with a larger key come first
+        for (int x = t; x < FX_SET; x += FX_NT)   // the distinct keys, compacted
+            if (scnt[x]) {
+                const uint32_t e = atomicAdd(&nd, 1u);
+                if (e < FX_LIST) {
+                    lkey[e] = skey[x];
+                    lslot[e] = (uint32_t)x;
+                } else if (err) {
+                    atomicOr(err, 32u);
+                }
+            }
+        __syncthreads();
+        const uint32_t nl = nd < FX_LIST ? nd : FX_LIST;
+        for (uint32_t e = t; e < nl; e += FX_NT) {   // elements with a larger key come first
+            uint32_t before = 0;
+            for (uint32_t f = 0; f < nl; f++)
+                if (lkey[f] > lkey[e]) before += scnt[lslot[f]];
+            sstart[lslot[e]] = before;
+        }
+        __syncthreads();
+        for (uint32_t e = t; e < nl; e += FX_NT) scnt[lslot[e]] = 0;   // the running count of placed elements
+        __syncthreads();
+        if (t < 64) {   // one wave places the run in order, 64 elements per round: stable
+            const uint64_t lt = (t ? (1ull << t) - 1 : 0ull);
+            for (int64_t q0 = a; q0 < b; q0 += 64) {
+                const int64_t q = q0 + t;
+                const bool valid = q < b;
+                uint64_t k = 0;
+                int slot = -1;
+                if (valid) {
+                    k = kf[q];
+                    uint32_t h = (uint32_t)(k ^ (k >> 29)) & (FX_SET - 1);
+                    while (skey[h] != k) h = (h + 1) & (FX_SET - 1);
+                    slot = (int)h;
+                }
+                uint64_t peers = __ballot(valid);
+#pragma unroll
+                for (int bit = 0; bit < 10; bit++) {
+                    const uint64_t bb = __ballot((slot >> bit) & 1);
+                    peers &= ((slot >> bit) & 1) ? bb : ~bb;
+                }
+                if (valid) {
+                    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+                    const int64_t dst = a + sstart[slot] + scnt[slot] + rank;
+                    ka[dst] = k;
+                    va[dst] = vf[q];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                if (valid && (peers & lt) == 0) scnt[slot] += (uint32_t)__popcll(peers);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+        }
+        __syncthreads();
+        for (int64_t q = a + t; q < b; q += FX_NT) {
+            kf[q] = ka[q];
+            vf[q] = va[q];
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void k_copy_idx(const uint32_t* v0, const uint32_t* v1, const uint64_t* st, uint32_t* out, int64_t n,
                            const uint64_t* lb, uint32_t* err) {
     if (err && blockIdx.x == 0 && threadIdx.x == 0 && lb[OS_ERR]) atomicOr(err, 4u);
@@ -574,6 +761,8 @@ void TopkScratch::release() {
     tile_a.release();
     tile_b.release();
     small.release();
+    fx_list.release();
+    fx_mark.release();
 }
 
 // before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
@@ -673,9 +862,20 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.os.ensure(lb_words);
     SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
     hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
-    for (int p = 0; p < 8; p++)
+    for (int p = 0; p < OS_MAX_PASSES; p++)
         hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntiles), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p);
+    // exact order among keys that share their 32-bit prefix
+    if (s.fx_mark.cap < (size_t)m) {   // run claims carry this call's epoch: zeroed only when (re)allocated
+        s.fx_mark.ensure((size_t)m);
+        SB_HIP(hipMemsetAsync(s.fx_mark.p, 0, s.fx_mark.cap * 4, st));
+        s.fx_epoch = 0;
+    }
+    const uint32_t epoch = ++s.fx_epoch;
+    s.fx_list.ensure((size_t)m);
+    hipLaunchKernelGGL(k_fx_mark, dim3(grid_for(m, 256, 2048)), dim3(256), 0, st, s.k0.p, s.k1.p, m, stv, s.fx_list.p);
+    hipLaunchKernelGGL(k_fx_fix, dim3(64), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, stv, s.fx_list.p,
+                       s.fx_mark.p, epoch, err);
     hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
     return m;

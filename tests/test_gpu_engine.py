@@ -128,6 +128,29 @@ def test_device_topk_key_ranges():
             assert np.array_equal(got, exp.astype(np.uint32)), (n, keep, keys[:3])
 
 
+def test_device_topk_prefix_fixup():
+    """The sort orders 32-bit prefixes of the varying bits, then fixes runs of equal prefixes that hold
+    different keys: keys spanning > 32 bits where many differ only below the prefix, with heavy ties,
+    a hot value sharing its prefix with others, runs longer than a workgroup, and runs at both ends."""
+    rng = np.random.default_rng(21)
+    base = np.uint64(0x40E0_0000_0000_0000)
+    cases = []
+    hi = rng.integers(0, 2**12, 400_000).astype(np.uint64) << np.uint64(40)    # 52 varying bits
+    lo = rng.integers(0, 3, 400_000).astype(np.uint64) * np.uint64(7)          # below the 32-bit prefix
+    cases.append(base + hi + lo)
+    hot = np.concatenate([np.full(20_000, 5, np.uint64), np.full(3_000, 6, np.uint64), np.full(9_000, 4, np.uint64),
+                          rng.integers(0, 2**50, 30_000).astype(np.uint64)])
+    cases.append(base + hot[rng.permutation(len(hot))])                         # long mixed run + spread keys
+    few = rng.integers(0, 2**44, 64).astype(np.uint64)
+    cases.append(base + rng.choice(few, 250_000) + rng.integers(0, 2, 250_000).astype(np.uint64))
+    for keys in cases:
+        n = len(keys)
+        for keep in (n // 5, n, n + 1):
+            exp = np.lexsort((np.arange(n), ~keys))[:min(keep, n)]
+            got = device_topk(keys, keep)
+            assert np.array_equal(got, exp.astype(np.uint32)), (n, keep)
+
+
 # ---------------------------------------------------------------- whole solves
 def _run_pair(goal, heur, width, seed, use_heuristic=True, test_flags=0):
     from splendor_amd.engine import HEURISTIC_IDS
