@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 run() {
     local name=$1; shift
     timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" --output-format csv -d "$OUT/$name" -o run -- \
-        python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/$name.json" 2> "$OUT/$name.err"
+        python3 bench.py --no-cpu-baseline --steps 6 --warmup 0 > "$OUT/$name.json" 2> "$OUT/$name.err"
 }
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 run sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT

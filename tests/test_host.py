@@ -102,8 +102,27 @@ def test_color_enum():
     assert repr(Color.RED) == str(Color.RED)
 
 
-def test_custom_heuristic_fails_loudly(monkeypatch):
-    """User Python heuristics cannot run in the device scorer: the solve raises instead of degrading."""
+def test_custom_heuristic_routes_to_host_scored_engine(monkeypatch):
+    """A user-registered heuristic selects the host-scored engine mode (SB_HEUR_HOST); there is no CPU
+    fallback, so without a GPU the solve raises (tests/test_gpu_custom.py runs it on the device)."""
+    import torch
+
+    from splendor_amd import _lib
+    from splendor_amd import solver as S
+    seen = {}
+
+    class Spy:
+        def __init__(self, **kw):
+            seen.update(kw)
+            raise RuntimeError('stop')
+
     monkeypatch.setitem(HEURISTICS, 'mine', lambda s: 1.0)
-    with pytest.raises(NotImplementedError):
+    monkeypatch.setattr(S, 'BeamEngine', Spy)
+    with pytest.raises(RuntimeError, match='stop'):
         State.newgame().solve(goal_pts=3, use_heuristic=True, heuristic_name='mine', verbose=False)
+    assert seen['heuristic'] == _lib.SB_HEUR_HOST and seen['use_heuristic']
+    monkeypatch.undo()
+    if not torch.cuda.is_available():
+        monkeypatch.setitem(HEURISTICS, 'mine', lambda s: 1.0)
+        with pytest.raises(_lib.SplendorBeamError):
+            State.newgame().solve(goal_pts=3, use_heuristic=True, heuristic_name='mine', verbose=False)
