@@ -467,6 +467,10 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     __shared__ uint32_t s_tile;
     const int t = threadIdx.x, w = t >> 6;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(lb + OS_TICKET);
+    const int64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
+    // a block takes tiles by ticket (in order) until they run out: the grid may be smaller than the
+    // tile count (SB_OS_GRID), trading workgroup dispatches for tiles processed back to back
+    for (;;) {
     if (t == 0) s_tile = atomicAdd(&ticket[p], 1u);
     {
         uint32_t* c32 = reinterpret_cast<uint32_t*>(&cnt[0][0][0]);
@@ -474,6 +478,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
     }
     __syncthreads();
     const int64_t tile = s_tile;
+    if (tile >= ntiles) return;
     const int64_t base = tile * OS_TILE;
     const int shift = 8 * p;
     const uint64_t slo = st[ST_SLO], psh = st[ST_SH32];
@@ -562,6 +567,8 @@ __global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, u
             kout[o] = kk[r];
             vout[o] = vv[r];
         }
+    }
+    __syncthreads();   // the next tile rewrites cnt / sbase
     }
 }
 
@@ -862,8 +869,12 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.os.ensure(lb_words);
     SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
     hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
+#ifndef SB_OS_GRID
+#define SB_OS_GRID 1u << 20   // blocks per pass at most (tiles beyond are taken by ticket)
+#endif
+    const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
     for (int p = 0; p < OS_MAX_PASSES; p++)
-        hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntiles), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+        hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p);
     // exact order among keys that share their 32-bit prefix
     if (s.fx_mark.cap < (size_t)m) {   // run claims carry this call's epoch: zeroed only when (re)allocated
