@@ -30,7 +30,19 @@ constexpr int TK_IPT = 16;
 constexpr int TK_TILE = TK_NT * TK_IPT;   // 4096
 constexpr int SEL_D = 11;                 // select digit bits
 constexpr int SEL_BINS = 1 << SEL_D;
-constexpr int SEL_PASSES_C = 6;           // candidate passes: ceil(64 / 11) upper bound
+constexpr int SEL_PASSES_C = 6;
+#ifndef SB_SEL_PREPASS
+#define SB_SEL_PREPASS 1   // select digits resolved over all keys before the partition (after the first)
+#endif
+constexpr int SEL_PREPASS = SB_SEL_PREPASS;
+#ifndef SB_TK_COUNT_GRID
+#define SB_TK_COUNT_GRID 2048   // persistent count blocks (8 per CU)
+#endif
+constexpr int64_t TK_COUNT_GRID = SB_TK_COUNT_GRID;
+#ifndef SB_TK_WRITE_GRID
+#define SB_TK_WRITE_GRID 1 << 20   // partition blocks at most (tiles beyond are taken in grid strides)
+#endif
+constexpr int64_t TK_WRITE_GRID = SB_TK_WRITE_GRID;           // candidate passes: ceil(64 / 11) upper bound
 #ifndef SB_SORT_PREFIX_BITS
 #define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
 #endif
@@ -220,51 +232,84 @@ __global__ __launch_bounds__(TK_NT) void k_tk_pick_fused(uint64_t* st, int64_t n
     for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
 }
 
-// per-tile counts of elements above / equal to the resolved prefix
+// per-tile counts of elements above / equal to the resolved prefix.  A block takes tiles
+// blockIdx.x, + gridDim.x, ... (16 loads in flight per thread); a wave counts with ballots and the four
+// wave counts meet in LDS (double-buffered: one barrier per tile).
 __global__ __launch_bounds__(TK_NT) void k_tk_count(const uint64_t* __restrict__ keys, int64_t n_host,
                                                     const uint64_t* __restrict__ n_dev, const uint64_t* __restrict__ st,
                                                     uint32_t* __restrict__ gt, uint32_t* __restrict__ eq) {
-    __shared__ uint32_t lds[TK_NT / 64 + 1];
+    constexpr int NW = TK_NT / 64;
+    __shared__ uint32_t wc[2][2][NW];
     const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
     const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
-    const int64_t base = (int64_t)blockIdx.x * TK_TILE;
-    uint32_t a = 0, b = 0;
-    if (base < n) {
+    const int t = threadIdx.x, w = t >> 6;
+    const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
+    int buf = 0;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, buf ^= 1) {
+        const int64_t base = tile * TK_TILE;
+        uint64_t kk[TK_IPT];
 #pragma unroll
         for (int j = 0; j < TK_IPT; j++) {
-            const int64_t i = base + (int64_t)j * TK_NT + threadIdx.x;
-            if (i < n) {
-                const uint64_t hb = hi_bits(keys[i], sh);
-                a += hb > prefix;
-                b += hb == prefix;
-            }
+            const int64_t i = base + (int64_t)j * TK_NT + t;
+            kk[j] = i < n ? keys[i] : 0ull;
         }
-    }
-    uint32_t ta, tb;
-    block_excl_scan<TK_NT>(a, lds, &ta);
-    block_excl_scan<TK_NT>(b, lds, &tb);
-    if (threadIdx.x == 0) {
-        gt[blockIdx.x] = ta;
-        eq[blockIdx.x] = tb;
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int j = 0; j < TK_IPT; j++) {
+            const int64_t i = base + (int64_t)j * TK_NT + t;
+            const uint64_t hb = hi_bits(kk[j], sh);
+            a += (uint32_t)__popcll(__ballot(i < n && hb > prefix));
+            b += (uint32_t)__popcll(__ballot(i < n && hb == prefix));
+        }
+        if ((t & 63) == 0) {
+            wc[buf][0][w] = a;
+            wc[buf][1][w] = b;
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint32_t sa = 0, sb = 0;
+#pragma unroll
+            for (int x = 0; x < NW; x++) {
+                sa += wc[buf][0][x];
+                sb += wc[buf][1][x];
+            }
+            gt[tile] = sa;
+            eq[tile] = sb;
+        }
     }
 }
 
 // single workgroup: exclusive tile offsets for both classes; totals into st[slot_gt], st[slot_eq].
-// phase 2 also sets the output bases of groups 2 and 3.
-__global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uint32_t* __restrict__ eq, int64_t ntiles,
-                                                   uint64_t* st, int slot_gt, int slot_eq, int phase2) {
+// phase 2 also sets the output bases of groups 2 and 3.  Thread t scans SC_PER consecutive tiles in
+// registers; one workgroup scan per SC_PER * 1024 tiles.
+constexpr int SC_PER = 16;
+__global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uint32_t* __restrict__ eq, int64_t n_host,
+                                                   const uint64_t* __restrict__ n_dev, uint64_t* st, int slot_gt,
+                                                   int slot_eq, int phase2) {
     __shared__ uint32_t lds[1024 / 64 + 1];
+    const int64_t ntiles = ((n_dev ? (int64_t)*n_dev : n_host) + TK_TILE - 1) / TK_TILE;
     uint32_t cg = 0, ce = 0;
-    for (int64_t b = 0; b < ntiles; b += 1024) {
-        const int64_t i = b + threadIdx.x;
-        const uint32_t g = i < ntiles ? gt[i] : 0, e = i < ntiles ? eq[i] : 0;
-        uint32_t tg, te;
-        const uint32_t xg = block_excl_scan<1024>(g, lds, &tg) + cg;
-        const uint32_t xe = block_excl_scan<1024>(e, lds, &te) + ce;
-        if (i < ntiles) {
-            gt[i] = xg;
-            eq[i] = xe;
+    for (int64_t b = 0; b < ntiles; b += 1024 * SC_PER) {
+        const int64_t i0 = b + (int64_t)threadIdx.x * SC_PER;
+        uint32_t g[SC_PER], e[SC_PER], sg = 0, se = 0;
+#pragma unroll
+        for (int j = 0; j < SC_PER; j++) {
+            g[j] = i0 + j < ntiles ? gt[i0 + j] : 0u;
+            e[j] = i0 + j < ntiles ? eq[i0 + j] : 0u;
+            sg += g[j];
+            se += e[j];
         }
+        uint32_t tg, te;
+        uint32_t xg = block_excl_scan<1024>(sg, lds, &tg) + cg;
+        uint32_t xe = block_excl_scan<1024>(se, lds, &te) + ce;
+#pragma unroll
+        for (int j = 0; j < SC_PER; j++)
+            if (i0 + j < ntiles) {
+                gt[i0 + j] = xg;
+                eq[i0 + j] = xe;
+                xg += g[j];
+                xe += e[j];
+            }
         cg += tg;
         ce += te;
     }
@@ -280,7 +325,7 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
 
 // Order-preserving partition of a tile (4096 elements, striped: element r*256 + t is thread t's r-th):
 // all 16 keys of a thread are loaded up front; per round and wave a ballot per class; one scan over
-// the tile's 16 x 4 (round, wave) counts orders everything (two barriers per tile).
+// the tile's 16 x 4 (round, wave) counts orders everything.  A block takes tiles in grid strides.
 // Elements above the prefix -> (gk, gi) at *gbase + rank; equal ones -> (ek, ei) at *ebase + rank,
 // only the first *limit of them if limit is given.
 __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
@@ -293,56 +338,61 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
     constexpr int NW = TK_NT / 64;
     __shared__ uint32_t cnt[TK_IPT * NW];   // (round, wave): above | equal << 16, then exclusive offsets
     const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
-    const int64_t base = (int64_t)blockIdx.x * TK_TILE;
-    if (base >= n) return;
+    const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
-    uint64_t kk[TK_IPT];
-#pragma unroll
-    for (int r = 0; r < TK_IPT; r++) {
-        const int64_t i = base + (int64_t)r * TK_NT + t;
-        kk[r] = i < n ? keys[i] : 0ull;
-    }
-    uint32_t fg = 0, fe = 0;   // bit r: this thread's r-th element is above / equal
-#pragma unroll
-    for (int r = 0; r < TK_IPT; r++) {
-        const int64_t i = base + (int64_t)r * TK_NT + t;
-        const uint64_t hb = hi_bits(kk[r], sh);
-        const bool g = i < n && hb > prefix, e = i < n && hb == prefix;
-        fg |= (uint32_t)g << r;
-        fe |= (uint32_t)e << r;
-        const uint64_t bg = __ballot(g), be = __ballot(e);
-        if (l == 0) cnt[r * NW + w] = (uint32_t)__popcll(bg) | ((uint32_t)__popcll(be) << 16);
-    }
-    __syncthreads();
-    if (t < 64) {   // exclusive scan of the 64 packed counts (round-major = index order)
-        const uint32_t v = t < TK_IPT * NW ? cnt[t] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        if (t < TK_IPT * NW) cnt[t] = inc - v;
-    }
-    __syncthreads();
-    if (!(fg | fe)) return;
-    const uint64_t og = (gbase ? *gbase : 0) + gt_off[blockIdx.x];
-    const uint64_t oe = eq_off[blockIdx.x];   // rank among equal elements before this tile
     const uint64_t lim = limit ? *limit : ~0ull;
     const uint64_t eb = ebase ? *ebase : 0;
+    const uint64_t gb = gbase ? *gbase : 0;
     const uint64_t lt = lanemask_lt();
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t base = tile * TK_TILE;
+        uint64_t kk[TK_IPT];
 #pragma unroll
-    for (int r = 0; r < TK_IPT; r++) {
-        const uint64_t bg = __ballot((fg >> r) & 1), be = __ballot((fe >> r) & 1);
-        const int64_t i = base + (int64_t)r * TK_NT + t;
-        const uint32_t c = cnt[r * NW + w];
-        if ((fg >> r) & 1) {
-            const uint64_t o = og + (c & 0xFFFFu) + __popcll(bg & lt);
-            gk[o] = kk[r];
-            gi[o] = idx ? idx[i] : (uint32_t)i;
-        } else if ((fe >> r) & 1) {
-            const uint64_t re = oe + (c >> 16) + __popcll(be & lt);
-            if (re < lim) {
-                ek[eb + re] = kk[r];
-                ei[eb + re] = idx ? idx[i] : (uint32_t)i;
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            kk[r] = i < n ? keys[i] : 0ull;
+        }
+        uint32_t fg = 0, fe = 0;   // bit r: this thread's r-th element is above / equal
+#pragma unroll
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            const uint64_t hb = hi_bits(kk[r], sh);
+            const bool g = i < n && hb > prefix, e = i < n && hb == prefix;
+            fg |= (uint32_t)g << r;
+            fe |= (uint32_t)e << r;
+            const uint64_t bg = __ballot(g), be = __ballot(e);
+            if (l == 0) cnt[r * NW + w] = (uint32_t)__popcll(bg) | ((uint32_t)__popcll(be) << 16);
+        }
+        __syncthreads();
+        if (t < 64) {   // exclusive scan of the 64 packed counts (round-major = index order)
+            const uint32_t v = t < TK_IPT * NW ? cnt[t] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (t < TK_IPT * NW) cnt[t] = inc - v;
+        }
+        __syncthreads();
+        if (fg | fe) {
+            const uint64_t og = gb + gt_off[tile];
+            const uint64_t oe = eq_off[tile];   // rank among equal elements before this tile
+#pragma unroll
+            for (int r = 0; r < TK_IPT; r++) {
+                const uint64_t bg = __ballot((fg >> r) & 1), be = __ballot((fe >> r) & 1);
+                const int64_t i = base + (int64_t)r * TK_NT + t;
+                const uint32_t c = cnt[r * NW + w];
+                if ((fg >> r) & 1) {
+                    const uint64_t o = og + (c & 0xFFFFu) + __popcll(bg & lt);
+                    gk[o] = kk[r];
+                    gi[o] = idx ? idx[i] : (uint32_t)i;
+                } else if ((fe >> r) & 1) {
+                    const uint64_t re = oe + (c >> 16) + __popcll(be & lt);
+                    if (re < lim) {
+                        ek[eb + re] = kk[r];
+                        ei[eb + re] = idx ? idx[i] : (uint32_t)i;
+                    }
+                }
             }
         }
+        __syncthreads();   // the next tile rewrites cnt
     }
 }
 
@@ -382,8 +432,19 @@ constexpr int OS_NT = 256;
 #define SB_OS_IPT 16
 #endif
 constexpr int OS_IPT = SB_OS_IPT;
-constexpr int OS_TILE = OS_NT * OS_IPT;   // 4096
-constexpr int OS_NW = OS_NT / 64;
+#ifndef SB_OS_PNT
+#define SB_OS_PNT 256    // threads per sort-pass workgroup (one tile of OS_PNT * OS_IPT elements)
+#endif
+constexpr int OS_PNT = SB_OS_PNT;
+constexpr int OS_TILE = OS_PNT * OS_IPT;
+constexpr int OS_NW = OS_PNT / 64;   // waves per pass workgroup
+#ifndef SB_OS_LB
+#define SB_OS_LB 8       // predecessors polled together per look-back round
+#endif
+constexpr int OS_LB = SB_OS_LB;
+#ifndef SB_OS_DBG
+#define SB_OS_DBG 0      // timing diagnostics only (wrong order): 1 no look-back, 2 unscattered writes
+#endif
 constexpr uint64_t OS_AGG = 1ull << 32, OS_INC = 2ull << 32;
 constexpr uint32_t OS_SPIN_MAX = 1u << 26;
 // control words at the start of the look-back buffer (u64): [0, 2048) histograms (u32 pairs), tickets
@@ -412,7 +473,7 @@ __device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64
 #ifndef SB_OSH_WH
 #define SB_OSH_WH 1          // per-wave sub-histograms (less LDS atomic contention between waves)
 #endif
-constexpr int OSH_NH = SB_OSH_WH ? OS_NW : 1;
+constexpr int OSH_NH = SB_OSH_WH ? OS_NT / 64 : 1;
 __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
                                                    const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     __shared__ uint32_t hh[OSH_NH][8][256];
@@ -454,121 +515,128 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(OS_NT) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
+// the tile's global offsets per digit: exclusive scan over the earlier tiles' published counts (look
+// back over the predecessors, OS_LB granules polled together: add counts until the first inclusive one;
+// wait where a predecessor has not published yet) plus the global start of the digit
+__device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int p, uint32_t agg, int t) {
+    const uint64_t ep = (uint64_t)(p + 1) << 34;
+    uint64_t* mine = lb + OS_HDR + tile * 256 + t;
+    uint32_t excl = 0;
+    if (tile == 0 || (SB_OS_DBG & 1)) {   // DBG 1 (timing only): no look-back
+        os_publish(mine, ep | OS_INC | agg);
+        return 0;
+    }
+    os_publish(mine, ep | OS_AGG | agg);
+    int64_t j = tile - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        uint64_t v[OS_LB];
+#pragma unroll
+        for (int u = 0; u < OS_LB; u++) v[u] = j - u >= 0 ? os_poll(lb + OS_HDR + (j - u) * 256 + t) : (ep | OS_INC);
+        int u = 0;
+        bool done = false;
+        for (; u < OS_LB; u++) {
+            if ((v[u] >> 34) != (uint64_t)(p + 1)) break;
+            excl += (uint32_t)v[u];
+            if (v[u] & OS_INC) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        j -= u;
+        if (u < OS_LB && ++spins > OS_SPIN_MAX) {   // bounded: a lost predecessor shows up as an error, not a hang
+            atomicOr(reinterpret_cast<uint32_t*>(lb + OS_ERR), 1u);
+            break;
+        }
+    }
+    os_publish(mine, ep | OS_INC | (uint64_t)(excl + agg));
+    return excl;
+}
+
+// Wave-sequential ranking: wave w owns the contiguous sub-tile [w * 64 * OS_IPT, (w + 1) * 64 * OS_IPT) of
+// the tile and walks it 64 elements per round (coalesced loads); per round a wave match (8 ballots) groups
+// equal digits, the group leader adds the group size to the wave's running count of that digit (an LDS
+// atomic that returns the count before) and the group shares it — the element's rank among the wave's
+// equal digits in index order.  A digit's offset in the tile is the sum of the earlier waves' counts.
+__global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
                                                    int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     if (p >= sort_passes(st)) return;
     const uint64_t* kin = (p & 1) ? k1 : k0;
     const uint32_t* vin = (p & 1) ? v1 : v0;
     uint64_t* kout = (p & 1) ? k0 : k1;
     uint32_t* vout = (p & 1) ? v0 : v1;
-    __shared__ uint16_t cnt[OS_IPT][OS_NW][256];   // (round, wave) counts per digit, then exclusive offsets
+    __shared__ uint32_t wcnt[OS_NW][256];   // running digit counts per wave, then exclusive offsets in the tile
     __shared__ uint32_t sbase[256];
     __shared__ uint32_t lds[OS_NW + 1];
     __shared__ uint32_t s_tile;
-    const int t = threadIdx.x, w = t >> 6;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(lb + OS_TICKET);
     const int64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
-    // a block takes tiles by ticket (in order) until they run out: the grid may be smaller than the
-    // tile count (SB_OS_GRID), trading workgroup dispatches for tiles processed back to back
-    for (;;) {
-    if (t == 0) s_tile = atomicAdd(&ticket[p], 1u);
-    {
-        uint32_t* c32 = reinterpret_cast<uint32_t*>(&cnt[0][0][0]);
-        for (int i = t; i < OS_IPT * OS_NW * 128; i += OS_NT) c32[i] = 0;
-    }
-    __syncthreads();
-    const int64_t tile = s_tile;
-    if (tile >= ntiles) return;
-    const int64_t base = tile * OS_TILE;
     const int shift = 8 * p;
     const uint64_t slo = st[ST_SLO], psh = st[ST_SH32];
     const uint64_t lt = lanemask_lt();
-    uint64_t kk[OS_IPT];
-    uint32_t vv[OS_IPT];
-    uint32_t rk[OS_IPT];   // digit | lane rank << 8
-#pragma unroll
-    for (int r = 0; r < OS_IPT; r++) {
-        const int64_t i = base + (int64_t)r * OS_NT + t;
-        kk[r] = i < n ? kin[i] : 0ull;
-        vv[r] = i < n ? vin[i] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < OS_IPT; r++) {
-        const int64_t i = base + (int64_t)r * OS_NT + t;
-        const bool valid = i < n;
-        const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & 255);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const uint64_t bb = __ballot((d >> b) & 1);
-            peers &= ((d >> b) & 1) ? bb : ~bb;
-        }
-        const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        if (valid && rank == 0) cnt[r][w][d] = (uint16_t)__popcll(peers);
-        rk[r] = d | (rank << 8);
-    }
-    __syncthreads();
-    // thread t owns digit t: exclusive offsets over (round, wave) in index order, tile aggregate
-    uint32_t agg = 0;
-#pragma unroll
-    for (int r = 0; r < OS_IPT; r++)
-#pragma unroll
-        for (int x = 0; x < OS_NW; x++) {
-            const uint32_t c = cnt[r][x][t];
-            cnt[r][x][t] = (uint16_t)agg;
-            agg += c;
-        }
-    const uint64_t ep = (uint64_t)(p + 1) << 34;
-    uint64_t* mine = lb + OS_HDR + tile * 256 + t;
-    uint32_t excl = 0;
-    if (tile == 0) {
-        os_publish(mine, ep | OS_INC | agg);
-    } else {
-        os_publish(mine, ep | OS_AGG | agg);
-        // look back over the predecessors, eight granules polled together: add counts until the first
-        // inclusive one; wait where a predecessor has not published yet
-        int64_t j = tile - 1;
-        uint32_t spins = 0;
-        for (;;) {
-            uint64_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = j - u >= 0 ? os_poll(lb + OS_HDR + (j - u) * 256 + t) : (ep | OS_INC);
-            int u = 0;
-            bool done = false;
-            for (; u < 8; u++) {
-                if ((v[u] >> 34) != (uint64_t)(p + 1)) break;
-                excl += (uint32_t)v[u];
-                if (v[u] & OS_INC) {
-                    done = true;
-                    break;
-                }
-            }
-            if (done) break;
-            j -= u;
-            if (u < 8 && ++spins > OS_SPIN_MAX) {   // bounded: a lost predecessor shows up as an error, not a hang
-                atomicOr(reinterpret_cast<uint32_t*>(lb + OS_ERR), 1u);
-                break;
-            }
-        }
-        os_publish(mine, ep | OS_INC | (uint64_t)(excl + agg));
-    }
-    // global start of each digit: exclusive scan of this pass's histogram
     const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * 256;
-    uint32_t tot;
-    const uint32_t gstart = block_excl_scan<OS_NT>(gh[t], lds, &tot);
-    sbase[t] = gstart + excl;
-    __syncthreads();
+    for (int it = 0;; it++) {
+        if (t == 0) s_tile = (SB_OS_DBG & 4) ? (it ? 0xFFFFFFFFu : blockIdx.x) : atomicAdd(&ticket[p], 1u);   // DBG 4: block order
+        for (int i = t; i < OS_NW * 256; i += OS_PNT) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        const int64_t tile = s_tile;
+        if (tile >= ntiles) return;
+        const int64_t base = tile * OS_TILE + (int64_t)w * (64 * OS_IPT) + l;
+        uint64_t kk[OS_IPT];
+        uint32_t vv[OS_IPT];
+        uint32_t rk[OS_IPT];   // digit | rank among the wave's equal digits << 8
 #pragma unroll
-    for (int r = 0; r < OS_IPT; r++) {
-        const int64_t i = base + (int64_t)r * OS_NT + t;
-        if (i < n) {
-            const uint32_t d = rk[r] & 255;
-            const uint32_t o = sbase[d] + cnt[r][w][d] + (rk[r] >> 8);
-            kout[o] = kk[r];
-            vout[o] = vv[r];
+        for (int r = 0; r < OS_IPT; r++) {
+            const int64_t i = base + (int64_t)r * 64;
+            kk[r] = i < n ? kin[i] : 0ull;
+            vv[r] = i < n ? vin[i] : 0u;
         }
-    }
-    __syncthreads();   // the next tile rewrites cnt / sbase
+#pragma unroll
+        for (int r = 0; r < OS_IPT; r++) {
+            const bool valid = base + (int64_t)r * 64 < n;
+            const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & 255);
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const uint64_t bb = __ballot((d >> b) & 1);
+                peers &= ((d >> b) & 1) ? bb : ~bb;
+            }
+            const int leader = valid ? __builtin_ctzll(peers) : l;
+            uint32_t before = 0;
+            if (valid && leader == l) before = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
+            before = __shfl(before, leader, 64);
+            rk[r] = d | ((before + (uint32_t)__popcll(peers & lt)) << 8);
+        }
+        __syncthreads();
+        // thread t < 256 owns digit t: the waves' exclusive offsets and the tile aggregate
+        uint32_t excl = 0;
+        if (t < 256) {
+            uint32_t agg = 0;
+#pragma unroll
+            for (int x = 0; x < OS_NW; x++) {
+                const uint32_t c = wcnt[x][t];
+                wcnt[x][t] = agg;
+                agg += c;
+            }
+            excl = os_lookback(lb, tile, p, agg, t);
+        }
+        uint32_t tot;
+        const uint32_t gstart = block_excl_scan<OS_PNT>(t < 256 ? gh[t] : 0u, lds, &tot);
+        if (t < 256) sbase[t] = gstart + excl;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < OS_IPT; r++) {
+            const int64_t i = base + (int64_t)r * 64;
+            if (i < n) {
+                const uint32_t d = rk[r] & 255;
+                const uint32_t o = (SB_OS_DBG & 2) ? (uint32_t)i : sbase[d] + wcnt[w][d] + (rk[r] >> 8);
+                kout[o] = kk[r];
+                vout[o] = vv[r];
+            }
+        }
+        __syncthreads();   // the next tile rewrites wcnt / sbase
     }
 }
 
@@ -838,11 +906,20 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv, (int)fused);
         hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, (int)fused);
         hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, (int)fused);
-        hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
+        // more digits over all keys before the partition: the scores crowd into few first-pass bins (about
+        // half of C3's keys share the threshold's), so the partition would copy most keys as candidates
+        for (int e = 0; e < SEL_PREPASS; e++) {
+            hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, 0);
+            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
+        }
+        const unsigned cg = (unsigned)std::min<int64_t>(ntiles, TK_COUNT_GRID);
+        const unsigned wg = (unsigned)std::min<int64_t>(ntiles, TK_WRITE_GRID);
+        hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
                            stv, s.tile_a.p, s.tile_b.p);
-        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv, (int)ST_A,
+        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, (const uint64_t*)nullptr,
+                           stv, (int)ST_A,
                            (int)ST_NC, 0);
-        hipLaunchKernelGGL(k_tk_write, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, keys, (const uint32_t*)nullptr, n,
+        hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, keys, (const uint32_t*)nullptr, n,
                            (const uint64_t*)nullptr, stv, s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p,
                            (const uint64_t*)nullptr, s.ck.p, s.ci.p, (const uint64_t*)nullptr,
                            (const uint64_t*)nullptr);
@@ -853,16 +930,18 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
             hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
         }
         // candidates above T -> group 2, the first NEED ties -> group 3
-        hipLaunchKernelGGL(k_tk_count, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p,
-                           s.tile_b.p);
-        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, ntiles, stv, (int)ST_G2,
+        hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
+        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, nc, stv, (int)ST_G2,
                            (int)ST_E2, 1);
-        hipLaunchKernelGGL(k_tk_write, dim3((unsigned)ntiles), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
+        hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
                            s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
                            stv + ST_NEED);
     } else {
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m);
     }
+#ifdef SB_DBG_EMPTY   // diagnostic: extra empty launches (kernel boundary cost)
+    for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
+#endif
     hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
     const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
@@ -874,7 +953,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #endif
     const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
     for (int p = 0; p < OS_MAX_PASSES; p++)
-        hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+        hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p);
     // exact order among keys that share their 32-bit prefix
     if (s.fx_mark.cap < (size_t)m) {   // run claims carry this call's epoch: zeroed only when (re)allocated
@@ -885,7 +964,10 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     const uint32_t epoch = ++s.fx_epoch;
     s.fx_list.ensure((size_t)m);
     hipLaunchKernelGGL(k_fx_mark, dim3(grid_for(m, 256, 2048)), dim3(256), 0, st, s.k0.p, s.k1.p, m, stv, s.fx_list.p);
-    hipLaunchKernelGGL(k_fx_fix, dim3(64), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, stv, s.fx_list.p,
+#ifndef SB_FX_GRID
+#define SB_FX_GRID 64   // fix-up workgroups (each takes flagged positions until none are left)
+#endif
+    hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, stv, s.fx_list.p,
                        s.fx_mark.p, epoch, err);
     hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
