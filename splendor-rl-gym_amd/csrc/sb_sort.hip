@@ -30,11 +30,17 @@ constexpr int TK_IPT = 16;
 constexpr int TK_TILE = TK_NT * TK_IPT;   // 4096
 constexpr int SEL_D = 11;                 // select digit bits
 constexpr int SEL_BINS = 1 << SEL_D;
-constexpr int SEL_PASSES_C = 6;
 #ifndef SB_SEL_PREPASS
 #define SB_SEL_PREPASS 1   // select digits resolved over all keys before the partition (after the first)
 #endif
 constexpr int SEL_PREPASS = SB_SEL_PREPASS;
+constexpr int SEL_PASSES_C = (64 - SEL_D * (1 + SEL_PREPASS) + SEL_D - 1) / SEL_D;   // candidate passes, at most
+#ifndef SB_TKH_GRID
+#define SB_TKH_GRID 512    // select histogram blocks (fewer flushes of the 2048 bins; 2048: +30 us)
+#endif
+#ifndef SB_TKH_U
+#define SB_TKH_U 16        // select histogram loads in flight per thread
+#endif
 #ifndef SB_TK_COUNT_GRID
 #define SB_TK_COUNT_GRID 2048   // persistent count blocks (8 per CU)
 #endif
@@ -72,7 +78,7 @@ enum : int {
 
 __device__ __forceinline__ uint64_t hi_bits(uint64_t k, uint64_t sh) { return sh >= 64 ? 0ull : k >> sh; }
 
-__global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range, int fused) {
+__device__ __forceinline__ void tk_init_body(uint64_t* st, int64_t keep, int keep_range, int fused) {
     const int t = threadIdx.x;
     if (t < ST_HIST && (t > ST_MAX || !keep_range) && !(fused && t == ST_FBASE)) st[t] = 0;
     __syncthreads();
@@ -83,6 +89,7 @@ __global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range, int fused)
     if (!fused)
         for (int i = t; i < SEL_BINS; i += blockDim.x) st[ST_HIST + i] = 0;
 }
+__global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range, int fused) { tk_init_body(st, keep, keep_range, fused); }
 
 __global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
     __shared__ unsigned long long smin, smax;
@@ -107,14 +114,14 @@ __global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict_
 }
 
 // common high bits of all keys: SH = position above the highest differing bit
-__global__ void k_tk_setup(uint64_t* st, int only_fallback) {
-    if (only_fallback && !st[ST_FALLBACK]) return;
+__device__ __forceinline__ void tk_setup_body(uint64_t* st) {
     const uint64_t x = st[ST_MIN] ^ st[ST_MAX];
     const uint64_t top = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
     st[ST_SH] = top;
     st[ST_PREFIX] = hi_bits(st[ST_MIN], top);
     st[ST_DONE] = top == 0;   // all keys equal: the first `keep` in index order
 }
+__global__ void k_tk_setup(uint64_t* st) { tk_setup_body(st); }
 
 // histogram of the next digit over the elements matching the resolved prefix; n from n_dev if given
 __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
     const uint64_t d = sh < SEL_D ? sh : SEL_D;
     const uint64_t dmask = (1ull << d) - 1;
     const uint64_t lt = lanemask_lt();
-    constexpr int U = 8;   // loads in flight per thread
+    constexpr int U = SB_TKH_U;   // loads in flight per thread
     const int64_t stride = (int64_t)gridDim.x * TK_NT;
     for (int64_t i0 = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i0 < n; i0 += stride * U) {
         uint64_t kk[U];
@@ -199,7 +206,7 @@ __global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallba
 // First pass from the histogram the emission folded (bins of key >> 47 in [FBASE, FBASE + 2048), the
 // edge bins clamped): pick the bin holding the keep-th largest key.  An edge bin mixes prefixes, so a
 // threshold there (or a count that is not n) sets FALLBACK and the generic first pass runs instead.
-__global__ __launch_bounds__(TK_NT) void k_tk_pick_fused(uint64_t* st, int64_t n) {
+__device__ __forceinline__ void tk_pick_fused_body(uint64_t* st, int64_t n) {
     __shared__ uint32_t lds[TK_NT / 64 + 1];
     const int t = threadIdx.x;
     constexpr int PER = SEL_BINS / TK_NT;
@@ -230,6 +237,16 @@ __global__ __launch_bounds__(TK_NT) void k_tk_pick_fused(uint64_t* st, int64_t n
     }
     __syncthreads();
     for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
+}
+
+// the fused select's first kernel: state reset, the pick from the folded histogram and, when that is
+// unusable, the generic first pass's setup
+__global__ __launch_bounds__(TK_NT) void k_tk_begin_fused(uint64_t* st, int64_t keep, int64_t n) {
+    tk_init_body(st, keep, 1, 1);
+    __syncthreads();
+    tk_pick_fused_body(st, n);
+    __syncthreads();
+    if (threadIdx.x == 0 && st[ST_FALLBACK]) tk_setup_body(st);
 }
 
 // per-tile counts of elements above / equal to the resolved prefix.  A block takes tiles
@@ -889,21 +906,24 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.v1.ensure(m);
     s.small.ensure(ST_WORDS);
     uint64_t* stv = s.small.p;
-    hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(256), 0, st, stv, (int64_t)m, (int)range_ready, (int)fused);
-    if (!range_ready)
-        hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
     const bool selected = n > keep;
+    if (fused && selected) {
+        hipLaunchKernelGGL(k_tk_begin_fused, dim3(1), dim3(TK_NT), 0, st, stv, (int64_t)m, n);
+    } else {
+        hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(TK_NT), 0, st, stv, (int64_t)m, (int)range_ready, (int)fused);
+        if (!range_ready)
+            hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
+        if (selected) hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv);
+    }
     if (selected) {
         const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
         s.tile_a.ensure(ntiles);
         s.tile_b.ensure(ntiles);
         s.ck.ensure(n);
         s.ci.ensure(n);
-        const unsigned hg = grid_for(n, TK_NT * 16, 2048);
+        const unsigned hg = grid_for(n, TK_NT * 16, SB_TKH_GRID);
         // first digit over all keys (folded into the producer when fused, generic pass as fallback),
         // then partition: above -> output group 1, bucket -> candidates
-        if (fused) hipLaunchKernelGGL(k_tk_pick_fused, dim3(1), dim3(TK_NT), 0, st, stv, n);
-        hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv, (int)fused);
         hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, (int)fused);
         hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, (int)fused);
         // more digits over all keys before the partition: the scores crowd into few first-pass bins (about
