@@ -892,9 +892,16 @@ static void preallocate_dist(Engine& E) {
     E.npar.ensure(nu);
     E.skey.ensure(nu);
     E.dsel_c.ensure(nu);
+    // the joint select's tile counts, tie tiles and destinations grow with the turn's unique children:
+    // a mid-step regrowth (hipFree) waits for the device to drain (0.2-0.5 ms each, sbd_sel_compact /
+    // sbd_partition); tiles of 4096 keys (sb_dist.inc PT_TILE)
+    const size_t dtiles = nu / 4096 + 2;
+    E.dsel_t.ensure(dtiles);
+    E.digit.ensure(nu);
+    E.part_hist.ensure(dtiles * (size_t)std::max(1, (int)E.cfg.world_size) + 80 + 16 * 64);
     E.kidx.ensure(wl);
     E.rkey.ensure(wl);
-    topk_reserve(E.topk, (int64_t)wl, (int64_t)wl);
+    topk_reserve(E.topk, (int64_t)nu, (int64_t)wl);
     E.scan.tiles.ensure(nr / SCAN_TILE + 1);
     E.turn_mem.reserve(wl * 20 * 24);
 }

@@ -885,6 +885,12 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     s.tile_b.ensure(n / TK_TILE + 1);
     s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * 256);
     s.small.ensure(ST_WORDS);
+    s.fx_list.ensure((size_t)m);
+    if (s.fx_mark.cap < (size_t)m) {   // run marks start at epoch 0 (see topk_stable_desc)
+        s.fx_mark.ensure((size_t)m);
+        SB_HIP(hipMemset(s.fx_mark.p, 0, s.fx_mark.cap * 4));
+        s.fx_epoch = 0;
+    }
 }
 
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window) {
