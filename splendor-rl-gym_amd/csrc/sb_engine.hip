@@ -270,6 +270,10 @@ constexpr int XP_U = SB_XP_U;
 #endif
 constexpr int XP_NT = SB_XP_NT;       // 4 waves
 constexpr int XP_PAR = SB_XP_PAR;     // parents per block iteration (<= 32)
+#ifndef SB_XP_DQ
+#define SB_XP_DQ 4   // A/B profiles/r2_ab_expand_dq.txt: 1 / 2 / 4 -> k_expand 3.35 / 3.30 / 3.24 ms (3 rounds)
+#endif
+constexpr uint32_t XP_DQ = SB_XP_DQ;  // parent groups per work-counter add
 static_assert(XP_PAR <= 32 && (31 | ((NCARDS + 127) << 5)) <= 0xFFFF, "k_expand queue entries: 5-bit s, 16-bit entry");
 
 struct XpShared {
@@ -293,6 +297,7 @@ struct XpShared {
     uint32_t nqb, nqt, nraw;          // wave rarely mixes the two (a buy re-hashes its card tuple)
     uint32_t proff[XP_PAR];           // SH: first record of each parent
     uint32_t grp[3];                  // this, next and next-but-one parent group
+    uint32_t dq_next, dq_left;        // groups left from the last dequeue (XP_DQ per counter add)
 };
 
 // enumeration tables into LDS: cards, colour masks, affordability masks, pattern deltas
@@ -366,9 +371,20 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
     };
     // groups are handed out in rank order by a counter (not a grid stride), so claims run roughly in
     // tag order and fewer same-turn holders get displaced; each block fetches a group ahead
+    // XP_DQ consecutive groups per counter add: one counter word serialises its atomics (MI355X: ~88 per
+    // us), so fewer adds keep the dequeue off the expansion's critical path
+    auto next_group = [&]() -> uint32_t {
+        if (S.dq_left == 0) {
+            S.dq_next = atomicAdd(work, 1u) * XP_DQ;
+            S.dq_left = XP_DQ;
+        }
+        S.dq_left--;
+        return S.dq_next++;
+    };
     if (t == 0) {
-        S.grp[0] = atomicAdd(work, 1u);
-        S.grp[1] = atomicAdd(work, 1u);
+        S.dq_left = 0;
+        S.grp[0] = next_group();
+        S.grp[1] = next_group();
     }
     __syncthreads();
     int64_t base = (int64_t)S.grp[0] * XP_PAR, nxt = (int64_t)S.grp[1] * XP_PAR;
@@ -376,7 +392,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
     while (base < n) {
         if (t == 0) {
             S.nqb = S.nqt = 0;
-            S.grp[2] = atomicAdd(work, 1u);   // the group after next; read after the barrier below
+            S.grp[2] = next_group();   // the group after next; read after the barrier below
         }
         if (t < XP_PAR * 3) (&S.cmask[0][0])[t] = 0;
         if (t < XP_PAR) S.plo[t] = pf;

@@ -91,25 +91,45 @@ __device__ __forceinline__ void tk_init_body(uint64_t* st, int64_t keep, int kee
 }
 __global__ void k_tk_init(uint64_t* st, int64_t keep, int keep_range, int fused) { tk_init_body(st, keep, keep_range, fused); }
 
+#ifndef SB_MINMAX_GRID
+#define SB_MINMAX_GRID 256   // blocks: each ends with two atomics on the same two words (they serialise)
+#endif
 __global__ __launch_bounds__(TK_NT) void k_tk_minmax(const uint64_t* __restrict__ keys, int64_t n, uint64_t* st) {
-    __shared__ unsigned long long smin, smax;
-    if (threadIdx.x == 0) {
-        smin = ~0ull;
-        smax = 0;
-    }
-    __syncthreads();
+    __shared__ unsigned long long wmin[TK_NT / 64], wmax[TK_NT / 64];
     uint64_t lo = ~0ull, hi = 0;
-    for (int64_t i = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * TK_NT) {
-        const uint64_t k = keys[i];
-        lo = k < lo ? k : lo;
-        hi = k > hi ? k : hi;
+    constexpr int U = 8;   // independent loads in flight per thread
+    const int64_t stride = (int64_t)gridDim.x * TK_NT;
+    for (int64_t i0 = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i0 < n; i0 += stride * U) {
+        uint64_t kk[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) kk[u] = i0 + u * stride < n ? keys[i0 + u * stride] : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i0 + u * stride < n) {
+                lo = kk[u] < lo ? kk[u] : lo;
+                hi = kk[u] > hi ? kk[u] : hi;
+            }
     }
-    atomicMin(&smin, (unsigned long long)lo);
-    atomicMax(&smax, (unsigned long long)hi);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {   // wave reduction, then one value per wave
+        const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wmin[threadIdx.x >> 6] = lo;
+        wmax[threadIdx.x >> 6] = hi;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        atomicMin((unsigned long long*)&st[ST_MIN], smin);
-        atomicMax((unsigned long long*)&st[ST_MAX], smax);
+        for (int w = 1; w < TK_NT / 64; w++) {
+            lo = wmin[w] < lo ? wmin[w] : lo;
+            hi = wmax[w] > hi ? wmax[w] : hi;
+        }
+        if (hi >= lo) {   // the block saw keys
+            atomicMin((unsigned long long*)&st[ST_MIN], (unsigned long long)lo);
+            atomicMax((unsigned long long*)&st[ST_MAX], (unsigned long long)hi);
+        }
     }
 }
 
@@ -918,7 +938,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     } else {
         hipLaunchKernelGGL(k_tk_init, dim3(1), dim3(TK_NT), 0, st, stv, (int64_t)m, (int)range_ready, (int)fused);
         if (!range_ready)
-            hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, 2048)), dim3(TK_NT), 0, st, keys, n, stv);
+            hipLaunchKernelGGL(k_tk_minmax, dim3(grid_for(n, TK_NT * 8, SB_MINMAX_GRID)), dim3(TK_NT), 0, st, keys, n, stv);
         if (selected) hipLaunchKernelGGL(k_tk_setup, dim3(1), dim3(1), 0, st, stv);
     }
     if (selected) {
