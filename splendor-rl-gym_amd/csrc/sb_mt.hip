@@ -98,16 +98,23 @@ __global__ __launch_bounds__(MT_NT) void k_mt_write(const uint32_t* __restrict__
 // the segment, in order, to stage[b * L ..] and their count to counts[b] (fused accept compaction);
 // MODE 2 (count) only counts them; MODE 3 (checkpoint) counts per sub-segment of ck twists and saves
 // the window at the start of each sub-segment to out (sharded streams, see noise_shard_chunk).
+#ifndef SB_MT_GEN_NT
+#define SB_MT_GEN_NT 256   // threads per producer: 4 waves (640: one lane per word; more waves beside k_expand)
+#endif
+constexpr int MG_NT = SB_MT_GEN_NT;
+constexpr int MG_NW = MG_NT / 64;
+constexpr int MG_R = (624 + MG_NT - 1) / MG_NT;   // words per thread in the temper / accept phase
+static_assert(MG_NT >= 227 && MG_NT % 64 == 0, "one mix phase per pass");
 template <int MODE>
-__global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
-                                                     uint8_t* __restrict__ stage, uint32_t* __restrict__ counts,
-                                                     int64_t twists, int ck = 1) {
+__global__ __launch_bounds__(MG_NT) void k_mt_gen_par(const uint32_t* __restrict__ wins, uint32_t* __restrict__ out,
+                                                       uint8_t* __restrict__ stage, uint32_t* __restrict__ counts,
+                                                       int64_t twists, int ck = 1) {
     constexpr bool RAW = MODE == 0;
     __shared__ uint32_t buf[2][624];
-    __shared__ uint32_t wc[10];
+    __shared__ uint32_t wc[MG_R][MG_NW];
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const int64_t b = blockIdx.x;
-    if (t < 624) buf[0][t] = wins[b * 624 + t];
+    for (int i = t; i < 624; i += MG_NT) buf[0][i] = wins[b * 624 + i];
     __syncthreads();
     uint32_t* o = RAW ? out + b * twists * 624 : nullptr;
     uint8_t* sg = RAW ? nullptr : stage + b * twists * 624;
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
         uint32_t* A = buf[cur];
         uint32_t* B = buf[cur ^ 1];
         if (MODE == 3 && w % ck == 0) {   // sub-segment boundary: its window, the previous one's count
-            if (t < 624) out[(b * nsub + w / ck) * 624 + t] = A[t];
+            for (int i = t; i < 624; i += MG_NT) out[(b * nsub + w / ck) * 624 + i] = A[i];
             if (t == 0 && w > 0) counts[b * nsub + w / ck - 1] = run;
             run = 0;
         }
@@ -129,23 +136,37 @@ __global__ __launch_bounds__(640) void k_mt_gen_par(const uint32_t* __restrict__
         if (t < 169) B[454 + t] = mt_mix(A[454 + t], A[455 + t], B[227 + t]);
         else if (t == 169) B[623] = mt_mix(A[623], B[0], B[396]);
         __syncthreads();
-        const uint32_t y = t < 624 ? mt_temper(B[t]) : 0u;
-        if (RAW) {
-            if (t < 624) o[w * 624 + t] = y;
-        } else {
-            const bool acc = t < 624 && (y >> 25) < 100u;
-            const uint64_t m = __ballot(acc);
-            if (lane == 0) wc[wv] = __popcll(m);
-            __syncthreads();
-            uint32_t before = 0, total = 0;
+        uint32_t y[MG_R];
 #pragma unroll
-            for (int x = 0; x < 10; x++) {
-                const uint32_t c = wc[x];
-                before += x < wv ? c : 0u;
-                total += c;
+        for (int r = 0; r < MG_R; r++) y[r] = r * MG_NT + t < 624 ? mt_temper(B[r * MG_NT + t]) : 0u;
+        if (RAW) {
+#pragma unroll
+            for (int r = 0; r < MG_R; r++)
+                if (r * MG_NT + t < 624) o[w * 624 + r * MG_NT + t] = y[r];
+        } else {
+            // accepted words in word order: round r (words r*NT + t), then wave, then lane
+            uint64_t m[MG_R];
+#pragma unroll
+            for (int r = 0; r < MG_R; r++) {
+                m[r] = __ballot(r * MG_NT + t < 624 && (y[r] >> 25) < 100u);
+                if (lane == 0) wc[r][wv] = (uint32_t)__popcll(m[r]);
             }
-            if (MODE == 1 && acc) sg[run + before + __popcll(m & lanemask_lt())] = (uint8_t)((y >> 25) + 1);
-            run += total;
+            __syncthreads();
+            uint32_t before = 0;
+#pragma unroll
+            for (int r = 0; r < MG_R; r++) {
+                uint32_t rb = 0, rt = 0;
+#pragma unroll
+                for (int x = 0; x < MG_NW; x++) {
+                    const uint32_t c = wc[r][x];
+                    rb += x < wv ? c : 0u;
+                    rt += c;
+                }
+                const bool acc = (m[r] >> lane) & 1;
+                if (MODE == 1 && acc) sg[run + before + rb + __popcll(m[r] & lanemask_lt())] = (uint8_t)((y[r] >> 25) + 1);
+                before += rt;
+            }
+            run += before;
         }
         cur ^= 1;
     }
@@ -281,7 +302,7 @@ void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipS
 void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
     if (chunk > 0)   // every producer jumps P*L ahead of its previous segment start
         hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
-    hipLaunchKernelGGL(k_mt_gen_par<0>, dim3(P), dim3(640), 0, st, d_win, out, (uint8_t*)nullptr,
+    hipLaunchKernelGGL(k_mt_gen_par<0>, dim3(P), dim3(MG_NT), 0, st, d_win, out, (uint8_t*)nullptr,
                        (uint32_t*)nullptr, twists);
     SB_HIP(hipGetLastError());
     chunk++;
@@ -290,7 +311,7 @@ void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
 void MTProducers::gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st) {
     if (chunk > 0)
         hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
-    hipLaunchKernelGGL(k_mt_gen_par<1>, dim3(P), dim3(640), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
+    hipLaunchKernelGGL(k_mt_gen_par<1>, dim3(P), dim3(MG_NT), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
                        twists);
     SB_HIP(hipGetLastError());
     chunk++;
@@ -424,7 +445,7 @@ void noise_shard_chunk(NoiseStream& ns, int slot, uint32_t* d_counts, hipStream_
     SB_HIP(hipStreamWaitEvent(st_mt, ns.ev_main, 0));
     if (pr.chunk > 0)
         hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st_mt, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
-    hipLaunchKernelGGL(k_mt_gen_par<3>, dim3(pr.P), dim3(640), 0, st_mt, pr.d_win,
+    hipLaunchKernelGGL(k_mt_gen_par<3>, dim3(pr.P), dim3(MG_NT), 0, st_mt, pr.d_win,
                        ns.ckpt.p + (size_t)slot * pr.P * S * 624, (uint8_t*)nullptr, d_counts, pr.twists, ns.ck);
     SB_HIP(hipGetLastError());
     pr.chunk++;   // asynchronous: the caller synchronises st_mt before using d_counts or the slot
