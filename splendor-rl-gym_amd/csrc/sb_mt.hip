@@ -237,6 +237,74 @@ constexpr int JMP_NT = 1024;
 constexpr int JMP_PARTS = 8;               // poly split: 8 x 78 words
 constexpr int JMP_JG = 10;                 // 624 outputs in groups of 64
 
+#ifndef SB_MT_JUMP_ROLL
+#define SB_MT_JUMP_ROLL 1   // rolling-window jump: 19 KB of LDS (0: the whole sequence in 87 KB)
+#endif
+#if SB_MT_JUMP_ROLL
+// window src0+b -> window dst0+b advanced by J (gp = x^(J-1) mod phi as 624 u32).  In place is safe.
+// The sequence y is generated in a ring of JR_RING words, JR_S polynomial bits at a time: each block of
+// bits needs y over [i0 + 1, i0 + JR_S + 624]; wave w accumulates the outputs of groups w, w+4, w+8 in
+// registers.  Runs beside the step's kernels on the side stream: 87 KB of LDS per CU had held the
+// expansion and the select to fewer resident blocks while it ran.
+#ifndef SB_JR_NT
+#define SB_JR_NT 1024   // A/B profiles/r2_ab_mt_nt.txt: 256 / 640 / 1024 threads
+#endif
+constexpr int JR_NT = SB_JR_NT, JR_RING = 4096, JR_S = 1024;
+constexpr int JR_NW = JR_NT / 64, JR_Q = (JMP_JG + JR_NW - 1) / JR_NW;   // output groups per wave
+static_assert(JR_RING >= 2 * JR_S + 624 + 227 + 1, "ring holds the block being read and the next one");
+__global__ __launch_bounds__(JR_NT) void k_mt_jump(const uint32_t* win_in, uint32_t* win_out, int src0, int dst0,
+                                                    const uint32_t* __restrict__ gpoly) {
+    __shared__ uint32_t ring[JR_RING];
+    __shared__ uint32_t gp[624];
+    constexpr int M = JR_RING - 1;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int64_t src = src0 + blockIdx.x, dst = dst0 + blockIdx.x;
+    for (int i = t; i < 624; i += JR_NT) {
+        ring[i] = win_in[src * 624 + i];
+        gp[i] = gpoly[i];
+    }
+    __syncthreads();
+    int have = 624;   // y[0, have) generated
+    uint32_t acc[JR_Q];
+#pragma unroll
+    for (int q = 0; q < JR_Q; q++) acc[q] = 0u;
+    for (int i0 = 0; i0 < 19937; i0 += JR_S) {
+        const int need = i0 + JR_S + 625;   // y indices read by this block: [i0 + 1, i0 + JR_S + 624]
+        while (have < need) {   // y_{k+624} = f(y_k, y_{k+1}, y_{k+397}), 227 at a time
+            const int k = have - 624 + t;
+            if (t < 227) ring[(k + 624) & M] = mt_mix(ring[k & M], ring[(k + 1) & M], ring[(k + 397) & M]);
+            have += 227;
+            __syncthreads();
+        }
+        const int wend = (i0 + JR_S) / 32 < 624 ? (i0 + JR_S) / 32 : 624;
+#pragma unroll
+        for (int q = 0; q < JR_Q; q++) {
+            const int jg = w + JR_NW * q;
+            if (jg >= JMP_JG) break;
+            const int j = jg * 64 + lane;
+            const int jj = j < 624 ? j : 623;
+            uint32_t a = acc[q];
+            for (int wi = i0 / 32; wi < wend; wi++) {
+                uint32_t bits = gp[wi];   // wave-uniform
+                while (bits) {
+                    const int b = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    a ^= ring[(1 + wi * 32 + b + jj) & M];
+                }
+            }
+            acc[q] = a;
+        }
+        __syncthreads();   // the next block's generation overwrites slots read here
+    }
+#pragma unroll
+    for (int q = 0; q < JR_Q; q++) {
+        const int j = (w + JR_NW * q) * 64 + lane;
+        if (w + JR_NW * q < JMP_JG && j < 624) win_out[dst * 624 + j] = acc[q];
+    }
+}
+constexpr int JMP_LAUNCH_NT = JR_NT;
+#else
+constexpr int JMP_LAUNCH_NT = JMP_NT;
 // window src0+b -> window dst0+b advanced by J (gp = x^(J-1) mod phi as 624 u32).  In place is safe.
 __global__ __launch_bounds__(JMP_NT) void k_mt_jump(const uint32_t* win_in, uint32_t* win_out, int src0, int dst0,
                                                      const uint32_t* __restrict__ gpoly) {
@@ -275,6 +343,7 @@ __global__ __launch_bounds__(JMP_NT) void k_mt_jump(const uint32_t* win_in, uint
     __syncthreads();
     for (int i = t; i < 624; i += JMP_NT) win_out[dst * 624 + i] = res[i];
 }
+#endif
 
 void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipStream_t st) {
     if (P_ < 1 || (P_ & (P_ - 1))) throw HipError{hipErrorInvalidValue, "MT producers must be a power of two"};
@@ -293,7 +362,7 @@ void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipS
     SB_HIP(hipMemcpyAsync(d_poly, polys.data(), polys.size() * 4, hipMemcpyHostToDevice, st));
     SB_HIP(hipMemcpyAsync(d_win, origin, 624 * 4, hipMemcpyHostToDevice, st));
     for (int k = 0; k < levels; k++)   // doubling tree: windows [2^k, 2^(k+1)) from [0, 2^k)
-        hipLaunchKernelGGL(k_mt_jump, dim3(1u << k), dim3(JMP_NT), 0, st, d_win, d_win, 0, 1 << k,
+        hipLaunchKernelGGL(k_mt_jump, dim3(1u << k), dim3(JMP_LAUNCH_NT), 0, st, d_win, d_win, 0, 1 << k,
                            d_poly + (size_t)k * 624);
     chunk_poly = d_poly + (size_t)levels * 624;
     SB_HIP(hipGetLastError());
@@ -301,7 +370,7 @@ void MTProducers::init(const uint32_t origin[624], int P_, int64_t twists_, hipS
 
 void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
     if (chunk > 0)   // every producer jumps P*L ahead of its previous segment start
-        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
+        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_LAUNCH_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
     hipLaunchKernelGGL(k_mt_gen_par<0>, dim3(P), dim3(MG_NT), 0, st, d_win, out, (uint8_t*)nullptr,
                        (uint32_t*)nullptr, twists);
     SB_HIP(hipGetLastError());
@@ -310,7 +379,7 @@ void MTProducers::gen_chunk(uint32_t* out, hipStream_t st) {
 
 void MTProducers::gen_chunk_accepted(uint8_t* stage, uint32_t* counts, hipStream_t st) {
     if (chunk > 0)
-        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
+        hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(JMP_LAUNCH_NT), 0, st, d_win, d_win, 0, 0, chunk_poly);
     hipLaunchKernelGGL(k_mt_gen_par<1>, dim3(P), dim3(MG_NT), 0, st, d_win, (uint32_t*)nullptr, stage, counts,
                        twists);
     SB_HIP(hipGetLastError());
@@ -419,7 +488,7 @@ void noise_mt_state(NoiseStream& ns, uint32_t* out625) {
 void noise_shard_setup(NoiseStream& ns, int rank, int world, hipStream_t st) {
     MTProducers& pr = ns.prod;
     for (int k = 0; k < rank; k++)   // producers to chunk `rank`
-        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.chunk_poly);
+        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_LAUNCH_NT), 0, st, pr.d_win, pr.d_win, 0, 0, pr.chunk_poly);
     const uint64_t L = (uint64_t)pr.twists * 624;
     std::vector<uint32_t> w(624);
     gf2::to_words(gf2::jump_poly(L * (uint64_t)pr.P * (uint64_t)world), w.data());
@@ -444,7 +513,7 @@ void noise_shard_chunk(NoiseStream& ns, int slot, uint32_t* d_counts, hipStream_
     SB_HIP(hipEventRecord(ns.ev_main, st_main));   // earlier packs may still read the slot
     SB_HIP(hipStreamWaitEvent(st_mt, ns.ev_main, 0));
     if (pr.chunk > 0)
-        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_NT), 0, st_mt, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
+        hipLaunchKernelGGL(k_mt_jump, dim3(pr.P), dim3(JMP_LAUNCH_NT), 0, st_mt, pr.d_win, pr.d_win, 0, 0, pr.stride_poly);
     hipLaunchKernelGGL(k_mt_gen_par<3>, dim3(pr.P), dim3(MG_NT), 0, st_mt, pr.d_win,
                        ns.ckpt.p + (size_t)slot * pr.P * S * 624, (uint8_t*)nullptr, d_counts, pr.twists, ns.ck);
     SB_HIP(hipGetLastError());
