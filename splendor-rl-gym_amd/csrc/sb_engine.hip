@@ -1181,6 +1181,10 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
     out->noise_draws = E.noise.consumed;
     static const bool htrace = getenv("SB_HOST_TRACE") != nullptr;
     const double h3 = host_ms();
+#ifndef SB_MT_GATE
+#define SB_MT_GATE 1   // noise generation starts after this turn's gather: beside the next expansion, not the top-k
+#endif
+    if (SB_MT_GATE && heur && !host_scores) SB_HIP(hipEventRecord(E.ev[1], E.s));
     launch_front(E);   // the next turn's expansion follows the gather on the stream
     const double h4 = host_ms();
     if (htrace)
@@ -1189,8 +1193,10 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
                 E.h_small[4], E.h_small[5], E.h_small[6]);
     // noise for the next turns on the side stream, overlapping that (latency-bound) expansion:
     // keep about three steps of accepted draws ahead
-    if (heur && !host_scores && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n)
+    if (heur && !host_scores && E.noise.produced - E.noise.consumed < 3 * (uint64_t)nu + (uint64_t)n) {
+        if (SB_MT_GATE) SB_HIP(hipStreamWaitEvent(E.s_mt, E.ev[1], 0));
         noise_generate_async(E.noise, E.s_mt);
+    }
 }
 
 // device phase times of a completed turn (timing flag): expand, count+scan, host gap, emit, top-k,
