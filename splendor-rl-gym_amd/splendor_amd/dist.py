@@ -264,8 +264,14 @@ class ShardNoise:
             wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv])
         b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
-        # next round in the background (side stream) while the steps go on; gathered when needed
-        if self.pending is None and self.gen_total < A + N + 4 * N:   # >= 3 steps to generate it
+        self._ahead = A + N + 4 * N   # background() launches the next round below this mark
+
+    def background(self):
+        """Next round in the background (side stream) while the steps go on; gathered when needed.
+        Called once the turn's kernels are enqueued: the round's side-stream work waits for them
+        (noise_shard_chunk orders it after the engine stream's pending work), so it runs beside the
+        next expansion instead of the emission, select and sort."""
+        if self.pending is None and self.gen_total < getattr(self, '_ahead', 0):   # >= 3 steps to generate it
             self._launch()
 
 
@@ -457,6 +463,8 @@ class DistSolve:
             rrec = rec[:int(dest_counts.sum())]
         self._mark(st, 'a2a_kept')
         b.receive(rrec, self.heur)
+        if self.heur:
+            self.noise.background()
         b.expand_launch(c.world)   # the next turn's expansion overlaps its goal check
         self._turn_sync()
         self._mark(st, 'rebalance')
