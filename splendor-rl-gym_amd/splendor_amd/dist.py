@@ -78,6 +78,8 @@ class Comm:
         return out
 
     def allgather_int(self, v: int) -> np.ndarray:
+        if self.world == 1:
+            return np.array([int(v)], dtype=np.int64)
         t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
         return self._gather_flat(t).cpu().numpy().astype(np.int64)
 
@@ -154,9 +156,9 @@ class Comm:
         """(world, len) int64 array of every rank's equal-length int vector (host: over the gloo metadata
         group, no device work)."""
         a = np.ascontiguousarray(arr, dtype=np.int64)
+        if self.world == 1:   # nothing to exchange: no device round trip
+            return a.reshape(1, len(a))
         if host:
-            if self.world == 1:
-                return a.reshape(1, len(a))
             t = torch.from_numpy(a)
             out = [torch.empty_like(t) for _ in range(self.world)]
             dist.all_gather(out, t, group=self.meta)
