@@ -571,8 +571,20 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
         mhi[threadIdx.x] = T->colmask_hi[threadIdx.x];
     }
     __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t dd = ndesc[idx[i]];
+#ifndef SB_GATHER_PF
+#define SB_GATHER_PF 0   // A/B: prefetch the next descriptor of this thread while rebuilding the current one
+#endif
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t dnext = (SB_GATHER_PF && i0 < m) ? ndesc[idx[i0]] : 0;
+    for (int64_t i = i0; i < m; i += gstride) {
+        uint64_t dd;
+        if (SB_GATHER_PF) {
+            dd = dnext;
+            if (i + gstride < m) dnext = ndesc[idx[i + gstride]];
+        } else {
+            dd = ndesc[idx[i]];
+        }
         const uint32_t r = (uint32_t)(dd >> 8);
         const int dsc = (int)(dd & 255);
         const uint64_t lo = plo[r], hi = phi[r];
@@ -1167,8 +1179,11 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
     nt.par = (uint32_t*)E.turn_mem.alloc(m * 4);
     nt.n = m;
     SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
+#ifndef SB_GATHER_GRID
+#define SB_GATHER_GRID 4096   // blocks of the descriptor gather (each thread walks m / (256 * grid) kept states)
+#endif
     if (desc)   // emission wrote descriptors only: rebuild the kept states from their parents
-        hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
+        hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, SB_GATHER_GRID)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
                            cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8);
     else
         hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
