@@ -59,6 +59,9 @@ def parse():
     ap.add_argument('--dry-run', action='store_true',
                     help='launcher plumbing only (CPU, gloo): every rank joins the group, rank 0 prints the world; '
                          'no GPU call (tests/test_bench_launch.py)')
+    ap.add_argument('--lookahead-edges', action='store_true',
+                    help='time the window with the engine lookahead at its edges too (the first timed turn\'s '
+                         'expansion runs before the clock starts, the turn after the window\'s inside it)')
     ap.add_argument('--realistic', action='store_true',
                     help='config C4 instead: realistic 2-player goal 15 --shuffle, W=1M (a separate line, not the '
                          'headline metric)')
@@ -138,8 +141,9 @@ class Window:
     same seed up to the first saturated turn; `left` steps of its window remain.  `make()` builds a
     seeded engine; `step(e)` / `sync(e)` / `close(e)` drive it."""
 
-    def __init__(self, make, step, sync, close, first, length):
+    def __init__(self, make, step, sync, close, first, length, look=None):
         self.make, self._step, self._sync, self._close = make, step, sync, close
+        self.look = look   # look(e, on): sb_set_lookahead (None: the engine always launches ahead)
         self.first, self.length = first, length   # window turns first .. first+length-1
         self.eng, self.left, self.engines = None, 0, 0
 
@@ -151,9 +155,13 @@ class Window:
             self.eng = None
         self.eng = self.make()
         self.engines += 1
-        for _ in range(self.first):   # setup: turns 0 .. first-1
+        for t in range(self.first):   # setup: turns 0 .. first-1
+            if self.look and t == self.first - 1:   # the first window turn's expansion is timed with it
+                self.look(self.eng, False)
             r = self._step(self.eng)
             assert not r['done'], 'setup reached the goal'
+        if self.look:
+            self.look(self.eng, True)
         self.left = self.length
         self._sync(self.eng)
 
@@ -202,9 +210,15 @@ def timed_steps(win, steps, warmup, sync_all, on_segment=None):
         turn0 = win.first + win.length - win.left
         sync_all(win.eng)
         t0 = time.perf_counter()
-        seg = [win.step() for _ in range(n)]
+        seg = []
+        for i in range(n):
+            if win.look and i == n - 1:   # the segment's last step does not start the next turn's expansion
+                win.look(win.eng, False)
+            seg.append(win.step())
         sync_all(win.eng)
         total += time.perf_counter() - t0
+        if win.look:
+            win.look(win.eng, True)
         if on_segment:
             on_segment(win.eng, turn0, seg)
         per += seg
@@ -221,7 +235,8 @@ def run_single(args):
                           beam_width=args.width, mt_state625=random.getstate()[1], device=0, timing=True)
 
     first, length, turns = probe_window(make, lambda e: e.step(), lambda e: e.close(), args.width)
-    win = Window(make, lambda e: e.step(), lambda e: e.sync(), lambda e: e.close(), first, length)
+    win = Window(make, lambda e: e.step(), lambda e: e.sync(), lambda e: e.close(), first, length,
+                 look=None if args.lookahead_edges else (lambda e, on: e.set_lookahead(on)))
 
     def phases(eng, turn0, seg):   # device phase times (HIP events recorded on the engine's stream)
         for i, p in enumerate(seg):
@@ -343,7 +358,9 @@ def main():
         'config': {'workload': f'speedrun goal_pts={GOAL} -u -H {args.heuristic} beam_width={args.width} (C3)',
                    'beam_width': args.width, 'heuristic': args.heuristic, 'seed': args.seed,
                    'parallelism': 'single GPU', 'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
-                   'timed_turns': [first, first + length - 1], 'moves': turns},
+                   'timed_turns': [first, first + length - 1], 'moves': turns,
+                   'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
+                                        if args.lookahead_edges else 'exactly the timed turns\' own')},
         'phases_ms': phases,
         'roofline': {'bound': 'hbm', 'kernel': dom.replace('ms_', 'k_'), 'achieved': round(achieved, 2),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),

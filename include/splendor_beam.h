@@ -133,6 +133,12 @@ int sb_get_mt_state(sb_engine* e, uint32_t* out625);
 /* Block until all device work of the handle has finished. */
 int sb_sync(sb_engine* e);
 
+/* Lookahead (default on): sb_step launches the next turn's expansion before it returns.  Off: it does
+ * not, and the next sb_step launches that expansion itself — a benchmark that times an exact set of
+ * turns turns it off for the step before the first timed one and for the last timed one, so the timed
+ * region holds the expansions of exactly the turns it counts.  Results do not depend on it. */
+int sb_set_lookahead(sb_engine* e, int32_t on);
+
 /* Visited-set entries (len(trail)). */
 int sb_visited_size(sb_engine* e, uint64_t* out);
 

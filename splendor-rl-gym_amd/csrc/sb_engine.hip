@@ -801,6 +801,8 @@ struct Engine {
     int max_pts = 0;
     uint64_t last_nu = 0;
     int front_turn = -1;                    // turn whose front half (expand .. readback) is in flight
+    bool lookahead = true;                  // finish_turn launches the next front half (sb_set_lookahead)
+    int64_t lost_zero = 0;                  // lost[0 .. 3 * lost_zero) is known zero (the emission cleared it)
     std::vector<hipEvent_t> tev;            // per-turn timing events (TEV_RING x 7)
     Arena turn_mem;
     hipEvent_t ev[8] = {};
@@ -975,11 +977,17 @@ static void launch_front(Engine& E) {
     // the claims below must fit: worst case every raw child is a new key
     grow_table(E, E.tab, E.tab_mask, (double)E.visited + E.raw_ratio * (double)n);
     E.cand.ensure((size_t)n * 3);
+    const unsigned long long* lost_was = E.lost.p;
     E.lost.ensure((size_t)n * 3);
+    if (E.lost.p != lost_was) E.lost_zero = 0;   // reallocated
     E.cnt.ensure((size_t)n);
     E.off.ensure((size_t)n);
     SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
-    SB_HIP(hipMemsetAsync(E.lost.p, 0, (size_t)n * 24, E.s));
+    {
+        const int64_t z = std::min<int64_t>(E.lost_zero, n);
+        if (n > z) SB_HIP(hipMemsetAsync(E.lost.p + (size_t)z * 3, 0, (size_t)(n - z) * 24, E.s));
+        E.lost_zero = 0;   // the expansion below marks [0, n)
+    }
     SB_HIP(hipMemsetAsync(E.d_small + 2, 0, 6 * 4, E.s));   // claim statistics (SB_CLAIM_STATS builds): [2..8)
     SB_HIP(hipMemsetAsync(E.d_small + 264, 0, 4, E.s));     // k_expand's group counter
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
@@ -1138,6 +1146,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
 #undef EMIT_K
         E.noise.consumed += (uint64_t)nu;
     }
+    if (SB_EMIT_ZERO_LOST) E.lost_zero = n;   // k_emit_w cleared lost[0 .. 3n) after reading it
     if (timing) SB_HIP(hipEventRecord(ev[4], E.s));
     if (host) {   // the turn ends in sb_prune, once the caller has scored next_queue (sb_read_next)
         SB_HIP(hipGetLastError());
@@ -1200,7 +1209,7 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
 #define SB_MT_GATE 1   // noise generation starts after this turn's gather: beside the next expansion, not the top-k
 #endif
     if (SB_MT_GATE && heur && !host_scores) SB_HIP(hipEventRecord(E.ev[1], E.s));
-    launch_front(E);   // the next turn's expansion follows the gather on the stream
+    if (E.lookahead) launch_front(E);   // the next turn's expansion follows the gather on the stream
     const double h4 = host_ms();
     if (htrace)
         fprintf(stderr, "turn %d sync %.3f pre-emit %.3f back %.3f front %.3f | old %u ins %u dup_early %u dup_lost %u displaced %u\n",
@@ -1549,6 +1558,12 @@ int sb_path(sb_engine* h, uint64_t* lo, uint64_t* hi, int32_t cap, int32_t* len)
 int sb_get_mt_state(sb_engine* h, uint32_t* out625) {
     if (!h || !out625) return SB_ERR_ARG;
     noise_mt_state(h->E.noise, out625);
+    return SB_OK;
+}
+
+int sb_set_lookahead(sb_engine* h, int32_t on) {
+    if (!h) return SB_ERR_ARG;
+    h->E.lookahead = on != 0;
     return SB_OK;
 }
 

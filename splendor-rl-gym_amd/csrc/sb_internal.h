@@ -102,6 +102,8 @@ struct TopkScratch {
     DBuf<uint64_t> small;           // select state + histogram
     DBuf<uint32_t> fx_list;         // sort fix-up: flagged positions
     DBuf<uint32_t> fx_mark;         // sort fix-up: run claims (epoch stamps)
+    DBuf<uint32_t> osh_part;        // sort digit histograms: one row per k_os_hist block (two-stage flush)
+    DBuf<uint32_t> tkh_part;        // select histograms: one row per k_tk_hist block (two-stage flush)
     uint32_t fx_epoch = 0;
     void release();
 };

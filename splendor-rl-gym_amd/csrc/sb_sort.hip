@@ -144,8 +144,10 @@ __device__ __forceinline__ void tk_setup_body(uint64_t* st) {
 __global__ void k_tk_setup(uint64_t* st) { tk_setup_body(st); }
 
 // histogram of the next digit over the elements matching the resolved prefix; n from n_dev if given
+// part != nullptr: the block stores its row of SEL_BINS counts there (k_tk_hsum adds the rows up)
 __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
-                                                   const uint64_t* __restrict__ n_dev, uint64_t* st, int only_fallback) {
+                                                   const uint64_t* __restrict__ n_dev, uint64_t* st, int only_fallback,
+                                                   uint32_t* __restrict__ part) {
     if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
     __shared__ uint32_t h[TK_NT / 64][SEL_BINS];
     const int w = threadIdx.x >> 6;
@@ -182,8 +184,37 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
     __syncthreads();
     for (int b = threadIdx.x; b < SEL_BINS; b += TK_NT) {
         const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
-        if (c) atomicAdd((unsigned long long*)&st[ST_HIST + b], (unsigned long long)c);
+        if (part) part[(size_t)blockIdx.x * SEL_BINS + b] = c;
+        else if (c) atomicAdd((unsigned long long*)&st[ST_HIST + b], (unsigned long long)c);
     }
+}
+// column sums of k_tk_hist's rows: grid (SEL_BINS / 256, ceil(rows / 32)), thread = bin; one atomic
+// per (bin, 32 rows) instead of one per (block, bin).  A/B (SB_TKH_2STAGE): the extra launch costs more
+// than the flush atomics it removes (select +40 us), so the default flushes with atomics
+__global__ __launch_bounds__(256) void k_tk_hsum(const uint32_t* __restrict__ part, int rows, uint64_t* st,
+                                                 int only_fallback) {
+    if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
+    const int b = blockIdx.x * 256 + threadIdx.x, r0 = blockIdx.y * 32;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < 32; r++)
+        if (r0 + r < rows) c += part[(size_t)(r0 + r) * SEL_BINS + b];
+    if (c) atomicAdd((unsigned long long*)&st[ST_HIST + b], (unsigned long long)c);
+}
+#ifndef SB_TKH_2STAGE
+#define SB_TKH_2STAGE 0   // A/B: select +40 us (profiles/r2_ab_hist_flush.txt)
+#endif
+static void tk_hist(TopkScratch& s, hipStream_t st, const uint64_t* keys, int64_t n, const uint64_t* n_dev,
+                    uint64_t* stv, int only_fallback, unsigned grid) {
+    uint32_t* part = nullptr;
+    if (SB_TKH_2STAGE) {
+        s.tkh_part.ensure((size_t)grid * SEL_BINS);
+        part = s.tkh_part.p;
+    }
+    hipLaunchKernelGGL(k_tk_hist, dim3(grid), dim3(TK_NT), 0, st, keys, n, n_dev, stv, only_fallback, part);
+    if (part)
+        hipLaunchKernelGGL(k_tk_hsum, dim3(SEL_BINS / 256, (grid + 31) / 32), dim3(256), 0, st, part, (int)grid, stv,
+                           only_fallback);
 }
 
 // pick the bucket holding the need-th largest matching element; clears the histogram
@@ -511,8 +542,17 @@ __device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64
 #define SB_OSH_WH 1          // per-wave sub-histograms (less LDS atomic contention between waves)
 #endif
 constexpr int OSH_NH = SB_OSH_WH ? OS_NT / 64 : 1;
+// Flush of the blocks' histograms: one atomic per (block, bin).  The two-stage flush (SB_OSH_2STAGE:
+// each block stores its row of P*256 counts, k_os_hsum adds 32 rows per thread with one atomic per
+// (column, 32 rows)) was measured no faster: the same-address atomics are not what bounds k_os_hist.
+#ifndef SB_OSH_2STAGE
+#define SB_OSH_2STAGE 0   // A/B: no faster (profiles/r2_ab_hist_flush.txt)
+#endif
+constexpr int OSH_ROW = 8 * 256;     // u32 per block row (digits 0..7)
+constexpr int OSH_RCHUNK = 32;       // rows per k_os_hsum thread
 __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
-                                                   const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
+                                                   const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
+                                                   uint32_t* __restrict__ part) {
     __shared__ uint32_t hh[OSH_NH][8][256];
     const int P = sort_passes(st);
     const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
@@ -548,8 +588,21 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
         uint32_t c = 0;
 #pragma unroll
         for (int v = 0; v < OSH_NH; v++) c += (&hh[v][0][0])[i];
-        if (c) atomicAdd(&gh[i], c);
+        if (SB_OSH_2STAGE) part[(size_t)blockIdx.x * OSH_ROW + i] = c;
+        else if (c) atomicAdd(&gh[i], c);
     }
+}
+// column sums of the k_os_hist rows: grid (8, ceil(rows / OSH_RCHUNK)), thread = column
+__global__ __launch_bounds__(256) void k_os_hsum(const uint32_t* __restrict__ part, int rows,
+                                                 const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= sort_passes(st) * 256) return;
+    const int r0 = blockIdx.y * OSH_RCHUNK;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < OSH_RCHUNK; r++)
+        if (r0 + r < rows) c += part[(size_t)(r0 + r) * OSH_ROW + col];
+    if (c) atomicAdd(reinterpret_cast<uint32_t*>(lb) + col, c);
 }
 
 // the tile's global offsets per digit: exclusive scan over the earlier tiles' published counts (look
@@ -875,6 +928,8 @@ void TopkScratch::release() {
     small.release();
     fx_list.release();
     fx_mark.release();
+    osh_part.release();
+    tkh_part.release();
 }
 
 // before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
@@ -906,6 +961,8 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * 256);
     s.small.ensure(ST_WORDS);
     s.fx_list.ensure((size_t)m);
+    if (SB_OSH_2STAGE) s.osh_part.ensure((size_t)grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID) * OSH_ROW);
+    if (SB_TKH_2STAGE) s.tkh_part.ensure((size_t)grid_for(n, TK_NT * 16, SB_TKH_GRID) * SEL_BINS);
     if (s.fx_mark.cap < (size_t)m) {   // run marks start at epoch 0 (see topk_stable_desc)
         s.fx_mark.ensure((size_t)m);
         SB_HIP(hipMemset(s.fx_mark.p, 0, s.fx_mark.cap * 4));
@@ -950,12 +1007,12 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         const unsigned hg = grid_for(n, TK_NT * 16, SB_TKH_GRID);
         // first digit over all keys (folded into the producer when fused, generic pass as fallback),
         // then partition: above -> output group 1, bucket -> candidates
-        hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, (int)fused);
+        tk_hist(s, st, keys, n, nullptr, stv, (int)fused, hg);
         hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, (int)fused);
         // more digits over all keys before the partition: the scores crowd into few first-pass bins (about
         // half of C3's keys share the threshold's), so the partition would copy most keys as candidates
         for (int e = 0; e < SEL_PREPASS; e++) {
-            hipLaunchKernelGGL(k_tk_hist, dim3(hg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr, stv, 0);
+            tk_hist(s, st, keys, n, nullptr, stv, 0, hg);
             hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
         }
         const unsigned cg = (unsigned)std::min<int64_t>(ntiles, TK_COUNT_GRID);
@@ -972,7 +1029,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         // remaining digits on the candidates (device-side count; passes after DONE exit at once)
         const uint64_t* nc = stv + ST_NC;
         for (int pass = 0; pass < SEL_PASSES_C; pass++) {
-            hipLaunchKernelGGL(k_tk_hist, dim3(std::min(hg, 512u)), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, 0);
+            tk_hist(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, 512u));
             hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
         }
         // candidates above T -> group 2, the first NEED ties -> group 3
@@ -993,7 +1050,12 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
     s.os.ensure(lb_words);
     SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
-    hipLaunchKernelGGL(k_os_hist, dim3(grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID)), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p);
+    const unsigned ohg = grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID);
+    if (SB_OSH_2STAGE) s.osh_part.ensure((size_t)ohg * OSH_ROW);
+    hipLaunchKernelGGL(k_os_hist, dim3(ohg), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p, s.osh_part.p);
+    if (SB_OSH_2STAGE)
+        hipLaunchKernelGGL(k_os_hsum, dim3(8, (ohg + OSH_RCHUNK - 1) / OSH_RCHUNK), dim3(256), 0, st, s.osh_part.p,
+                           (int)ohg, stv, s.os.p);
 #ifndef SB_OS_GRID
 #define SB_OS_GRID 1u << 20   // blocks per pass at most (tiles beyond are taken by ticket)
 #endif

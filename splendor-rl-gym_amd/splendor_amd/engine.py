@@ -125,6 +125,10 @@ class BeamEngine:
     def sync(self):
         L.check(L.lib().sb_sync(self._h), 'sb_sync')
 
+    def set_lookahead(self, on):
+        """Launch the next turn's expansion at the end of step() (default) or at the start of the next."""
+        L.check(L.lib().sb_set_lookahead(self._h, int(bool(on))), 'sb_set_lookahead')
+
     def visited_size(self) -> int:
         v = C.c_uint64()
         L.check(L.lib().sb_visited_size(self._h, C.byref(v)))

@@ -274,3 +274,26 @@ def test_saved_overflow_is_an_error_not_a_clamp():
         for _ in range(3):
             eng.step()
     eng.close()
+
+
+def test_solve_lookahead_toggled_golden():
+    """sb_set_lookahead (the bench switches it at the edges of its timed window): with the next turn's
+    expansion launched at the end of a step or at the start of the next, in any pattern, the beams,
+    path and MT state stay the golden's."""
+    rng = np.random.default_rng(7)
+    for g in [golden('solve_g15_balanced_w300000_s0.json')] + golden('solves_small.json')[:4]:
+        eng, _ = _run_pair(g['goal'], g['heuristic'], g['beam_width'], g['seed'])
+        turns = [t for t in g['turns'] if t['n_unique'] > 0]
+        t = 0
+        while True:
+            eng.set_lookahead(bool(rng.integers(2)))
+            stt = eng.step()
+            if stt['done']:
+                break
+            t += 1
+            _, _, _, key = eng.read_turn(t)
+            assert oracle_c.beam_digest(key) == turns[t - 1]['digest'], f'turn {t}'
+        assert t == len(turns)
+        assert [_skey(a, b) for a, b in eng.path()] == [p[5] for p in g['path']]
+        assert oracle_c.mt_fingerprint(eng.mt_state()) == g['final_mt']
+        eng.close()
