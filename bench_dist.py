@@ -72,7 +72,8 @@ def main(args):
         dist.barrier()
 
     first, length, turns = probe_window(make, lambda s: s.step(), close, W)
-    win = Window(make, lambda s: s.step(), lambda s: torch.cuda.synchronize(), close, first, length)
+    win = Window(make, lambda s: s.step(), lambda s: torch.cuda.synchronize(), close, first, length,
+                 look=None if args.lookahead_edges else (lambda s, on: setattr(s, 'lookahead', on)))
     per, el = timed_steps(win, args.steps, args.warmup, sync_all)
     win.close()
     comm = Comm(torch.device('cuda', dev))
@@ -98,7 +99,9 @@ def main(args):
                        'beam_width': W, 'heuristic': args.heuristic, 'seed': args.seed,
                        'parallelism': f'beam sharded over {world} GPUs ({backend})',
                        'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
-                       'timed_turns': [first, first + length - 1], 'moves': turns},
+                       'timed_turns': [first, first + length - 1], 'moves': turns,
+                       'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
+                                            if args.lookahead_edges else 'exactly the timed turns\' own')},
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},

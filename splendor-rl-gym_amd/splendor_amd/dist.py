@@ -292,6 +292,8 @@ class DistSolve:
         self.winner = None                      # (turn, global rank)
         self.counts = []                        # per turn: per-rank slice sizes
         self.b.expand_launch(self.c.world)      # runs while the host does the turn sync / goal check
+        self.lookahead = True                   # step() launches the next turn's expansion before returning
+        self._front_deferred = False            # lookahead was off: the next step() launches it
         self._turn_sync()
         self.noise = ShardNoise(backend, comm) if use_heuristic else None
         self.consumed = 0                       # accepted draws used so far (global)
@@ -360,6 +362,9 @@ class DistSolve:
         # the expansion (launched when this slice arrived) claimed the own children; the records for the
         # other owners are partitioned by owner.  Exchange chunks: claims of chunk j overlap chunk j+1's transfer
         C = self.nchunk if st['n_parents'] * 24 >= self.chunk_min else 1
+        if self._front_deferred:
+            b.expand_launch(c.world)
+            self._front_deferred = False
         cc, n_raw = b.expand_counts(C)                              # (C, world) records per chunk, owner
         M = c.allgather_array(np.concatenate([cc.ravel(), [n_raw]]))
         st['n_raw'] = int(M[:, -1].sum())
@@ -467,7 +472,10 @@ class DistSolve:
         b.receive(rrec, self.heur)
         if self.heur:
             self.noise.background()
-        b.expand_launch(c.world)   # the next turn's expansion overlaps its goal check
+        if self.lookahead:
+            b.expand_launch(c.world)   # the next turn's expansion overlaps its goal check
+        else:   # a benchmark's window edge (bench.py): the next step() launches it
+            self._front_deferred = True
         self._turn_sync()
         self._mark(st, 'rebalance')
         self.turn += 1

@@ -48,7 +48,13 @@ def _worker(rank, world, port, cfg, outdir):
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
     solve = DistSolve(b, Comm(torch.device('cpu')), goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                       beam_width=cfg['width'])
-    trace = solve.run()
+    if cfg.get('toggle'):   # bench.py's window edges: the next turn's expansion deferred to the next step
+        trace = []
+        while not solve.done:
+            solve.lookahead = len(trace) % 3 != 1
+            trace.append(solve.step())
+    else:
+        trace = solve.run()
     out = {'trace': trace, 'counts': [c.tolist() for c in solve.counts], 'path': [list(x) for x in solve.path()],
            'slices': [[lo, hi, par] for lo, hi, par in b.turns],
            'mt': b.mt_state().tolist() if cfg['heur'] else None}
@@ -73,6 +79,8 @@ CASES = [
     # the driver's scaling runs use 4 and 8 ranks
     (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'chunks': 2}),
     (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True}),
+    # lookahead off every third step (the expansion launched by the step that needs it)
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True}),
 ]
 
 
