@@ -31,6 +31,8 @@ def main():
     ap.add_argument('dir')
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--out', required=True)
+    ap.add_argument('--edges', action='store_true',
+                    help='the run used bench.py --lookahead-edges (round-2 accounting before session 4)')
     a = ap.parse_args()
     def load(path, counter=None):
         """[(name, start, end, value)] in dispatch order (value = counter value for PMC files)."""
@@ -44,11 +46,15 @@ def main():
         return out
 
     def timed_window(recs):
-        """Dispatches of the timed turns: the expansion of the first timed turn is launched (pipelined)
-        inside the step before it, the expansion after the last timed turn inside the last timed step;
-        the timed turns' kernels lie between those two expansion starts."""
+        """Dispatches of the timed turns (one engine: bench.py --steps S --warmup 0).  Exact accounting
+        (default): the last S expansions are the timed turns' own and everything from the first of them
+        on is timed.  --edges: the first timed turn's expansion was launched inside the step before it
+        and the last timed step launched the next one: the window lies between those two starts."""
         ex = [r for r in recs if r[0].startswith('k_expand')]
-        t0, t1 = ex[-a.steps - 1][1], ex[-1][1]
+        if a.edges:
+            t0, t1 = ex[-a.steps - 1][1], ex[-1][1]
+        else:
+            t0, t1 = ex[-a.steps][1], float('inf')
         return [r for r in recs if t0 <= r[1] < t1]
 
     rows = load(os.path.join(a.dir, 'trace', 'run_kernel_trace.csv'))
