@@ -62,6 +62,9 @@ def parse():
     ap.add_argument('--lookahead-edges', action='store_true',
                     help='time the window with the engine lookahead at its edges too (the first timed turn\'s '
                          'expansion runs before the clock starts, the turn after the window\'s inside it)')
+    ap.add_argument('--sync-all-streams', action='store_true',
+                    help='end each timed segment with a sync of every stream, the noise generation running '
+                         'ahead for later turns included')
     ap.add_argument('--realistic', action='store_true',
                     help='config C4 instead: realistic 2-player goal 15 --shuffle, W=1M (a separate line, not the '
                          'headline metric)')
@@ -197,12 +200,19 @@ def probe_window(make, step, close, width):
     return first, last - first + 1, turn
 
 
-def timed_steps(win, steps, warmup, sync_all, on_segment=None):
+def timed_steps(win, steps, warmup, sync_all, on_segment=None, sync_end=None):
     """Warmup then exactly `steps` timed window steps, segment by segment (a segment ends where an
-    engine's window ends); returns (per-step stats, total seconds)."""
-    for _ in range(warmup):
+    engine's window ends); returns (per-step stats, total seconds).  Each segment starts with every
+    stream idle (sync_all) and ends when its turns' work is done (sync_end, default sync_all)."""
+    sync_end = sync_end or sync_all
+    for w in range(warmup):
         win.ensure()
+        last = w == warmup - 1 and win.left > 1   # the timed steps continue on this engine
+        if win.look and last:   # ... so the first timed turn's expansion is left to the first timed step
+            win.look(win.eng, False)
         win.step()
+        if win.look and last:
+            win.look(win.eng, True)
     per, total = [], 0.0
     while len(per) < steps:
         win.ensure()
@@ -215,12 +225,17 @@ def timed_steps(win, steps, warmup, sync_all, on_segment=None):
             if win.look and i == n - 1:   # the segment's last step does not start the next turn's expansion
                 win.look(win.eng, False)
             seg.append(win.step())
-        sync_all(win.eng)
-        total += time.perf_counter() - t0
+        sync_end(win.eng)
+        dt = time.perf_counter() - t0
+        total += dt
         if win.look:
             win.look(win.eng, True)
         if on_segment:
             on_segment(win.eng, turn0, seg)
+        if os.environ.get('SB_BENCH_SEGDBG'):
+            ev = sum(p.get('ms_total', 0.0) for p in seg)
+            print(f'segment turns {turn0}..{turn0 + n - 1}: wall {dt * 1e3:.3f} ms, device events {ev:.3f} ms',
+                  file=sys.stderr, flush=True)
         per += seg
     return per, total
 
@@ -242,7 +257,11 @@ def run_single(args):
         for i, p in enumerate(seg):
             p.update(eng.turn_times(turn0 + i))
 
-    per, elapsed = timed_steps(win, args.steps, args.warmup, lambda e: e.sync(), phases)
+    # the clock stops when the timed turns are done on the engine stream; the MT producers' chunk for
+    # later turns (launched ahead by the last step, overlapping the next expansion in a longer run) is
+    # not waited for (--sync-all-streams: it is)
+    per, elapsed = timed_steps(win, args.steps, args.warmup, lambda e: e.sync(), phases,
+                               sync_end=None if args.sync_all_streams else (lambda e: e.sync_engine()))
     win.close()
     return per, elapsed, (first, length, turns, win.engines)
 
@@ -360,7 +379,9 @@ def main():
                    'parallelism': 'single GPU', 'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
                    'timed_turns': [first, first + length - 1], 'moves': turns,
                    'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
-                                        if args.lookahead_edges else 'exactly the timed turns\' own')},
+                                        if args.lookahead_edges else 'exactly the timed turns\' own'),
+                   'segment_end': ('every stream' if args.sync_all_streams else
+                                   'the engine stream (noise generation for later turns not waited for)')},
         'phases_ms': phases,
         'roofline': {'bound': 'hbm', 'kernel': dom.replace('ms_', 'k_'), 'achieved': round(achieved, 2),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),

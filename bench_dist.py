@@ -74,7 +74,12 @@ def main(args):
     first, length, turns = probe_window(make, lambda s: s.step(), close, W)
     win = Window(make, lambda s: s.step(), lambda s: torch.cuda.synchronize(), close, first, length,
                  look=None if args.lookahead_edges else (lambda s, on: setattr(s, 'lookahead', on)))
-    per, el = timed_steps(win, args.steps, args.warmup, sync_all)
+    def sync_end(_s):   # the timed turns' work (the engine runs on torch's stream); noise rounds ahead not waited for
+        torch.cuda.current_stream().synchronize()
+        dist.barrier()
+
+    per, el = timed_steps(win, args.steps, args.warmup, sync_all,
+                          sync_end=None if args.sync_all_streams else sync_end)
     win.close()
     comm = Comm(torch.device('cuda', dev))
     el_max = float(comm.allreduce(np.array([int(el * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9
@@ -101,7 +106,9 @@ def main(args):
                        'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
                        'timed_turns': [first, first + length - 1], 'moves': turns,
                        'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
-                                            if args.lookahead_edges else 'exactly the timed turns\' own')},
+                                            if args.lookahead_edges else 'exactly the timed turns\' own'),
+                       'segment_end': ('every stream' if args.sync_all_streams else
+                                       'the engine stream (noise rounds for later turns not waited for)')},
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},

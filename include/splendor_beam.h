@@ -139,6 +139,10 @@ int sb_sync(sb_engine* e);
  * region holds the expansions of exactly the turns it counts.  Results do not depend on it. */
 int sb_set_lookahead(sb_engine* e, int32_t on);
 
+/* Block until the turns launched so far have finished on the engine stream; the noise generation that
+ * runs ahead of need on its own stream (draws for later turns) is not waited for.  sb_sync waits for both. */
+int sb_sync_engine(sb_engine* e);
+
 /* Visited-set entries (len(trail)). */
 int sb_visited_size(sb_engine* e, uint64_t* out);
 

@@ -1567,6 +1567,15 @@ int sb_set_lookahead(sb_engine* h, int32_t on) {
     return SB_OK;
 }
 
+int sb_sync_engine(sb_engine* h) {
+    if (!h) return SB_ERR_ARG;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(h->E.dev));
+        SB_HIP(hipStreamSynchronize(h->E.s));
+        return SB_OK;
+    });
+}
+
 int sb_sync(sb_engine* h) {
     if (!h) return SB_ERR_ARG;
     return guarded([&]() {

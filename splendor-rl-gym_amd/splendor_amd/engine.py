@@ -125,6 +125,10 @@ class BeamEngine:
     def sync(self):
         L.check(L.lib().sb_sync(self._h), 'sb_sync')
 
+    def sync_engine(self):
+        """Wait for the launched turns (engine stream), not for noise generation running ahead."""
+        L.check(L.lib().sb_sync_engine(self._h), 'sb_sync_engine')
+
     def set_lookahead(self, on):
         """Launch the next turn's expansion at the end of step() (default) or at the start of the next."""
         L.check(L.lib().sb_set_lookahead(self._h, int(bool(on))), 'sb_set_lookahead')
