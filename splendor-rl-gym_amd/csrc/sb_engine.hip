@@ -557,7 +557,7 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
                                                   const uint64_t* __restrict__ ndesc, const uint64_t* __restrict__ plo,
                                                   const uint64_t* __restrict__ phi, uint64_t* __restrict__ olo,
                                                   uint64_t* __restrict__ ohi, uint32_t* __restrict__ opar,
-                                                  uint32_t* __restrict__ first) {
+                                                  uint32_t* __restrict__ first, int desc_in_idx) {
     __shared__ uint32_t f[256];
     __shared__ uint32_t card[NCARDS];
     __shared__ int32_t pdelta[4][NPAT_MAX];
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
             dd = dnext;
             if (i + gstride < m) dnext = ndesc[idx[i + gstride]];
         } else {
-            dd = ndesc[idx[i]];
+            dd = desc_in_idx ? (uint64_t)idx[i] : ndesc[idx[i]];   // the top-k carried the descriptor itself
         }
         const uint32_t r = (uint32_t)(dd >> 8);
         const int dsc = (int)(dd & 255);
@@ -1168,6 +1168,11 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
     // ---- prune + next beam
     int64_t m = nu;
     uint32_t* idx = nullptr;
+#ifndef SB_TOPK_DESC
+#define SB_TOPK_DESC 1   // the top-k carries each kept survivor's descriptor (rank << 8 | dsc) instead of its index
+#endif
+    // descriptors fit the 32-bit payload while parent ranks < 2^24
+    const bool desc_pay = SB_TOPK_DESC && desc && heur && !host_scores && n < ((int64_t)1 << 24);
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
         if (host_scores) {   // f64 scores -> order-preserving u64 keys (a NaN sets error bit 16)
@@ -1177,7 +1182,7 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
                                  E.d_small + 1, /*fused=*/false);
         } else {
             m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true,
-                                 E.d_small + 1, /*fused=*/!(E.cfg.flags & 4));
+                                 E.d_small + 1, /*fused=*/!(E.cfg.flags & 4), desc_pay ? E.nlo.p : nullptr);
         }
         idx = E.kidx.p;
     }
@@ -1193,7 +1198,7 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
 #endif
     if (desc)   // emission wrote descriptors only: rebuild the kept states from their parents
         hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, SB_GATHER_GRID)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
-                           cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8);
+                           cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8, (int)desc_pay);
     else
         hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
                            nt.lo, nt.hi, nt.par, E.d_small + 8);
