@@ -1012,6 +1012,12 @@ static void launch_front(Engine& E) {
 }
 
 static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const double* host_scores, sb_step_stats* out);
+#ifndef SB_TOPK_DESC
+#define SB_TOPK_DESC 1   // the top-k carries each kept survivor's descriptor (rank << 8 | dsc) instead of its index
+#endif
+// descriptor-only emission writes 4-byte descriptors that the top-k carries as its payload while parent
+// ranks < 2^24 (else 8-byte descriptors and the gather reads them at the kept indices)
+static bool desc_payload_ok(int64_t n_parents) { return SB_TOPK_DESC && n_parents < ((int64_t)1 << 24); }
 static double host_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1121,7 +1127,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
         hipLaunchKernelGGL(EMIT_K(-1), dim3(eg), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, E.lost.p,
                            E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, rbase, 0u,
                            E.d_small + 1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                           (const uint64_t*)nullptr);
+                           (const uint64_t*)nullptr, 0);
     } else {
         const bool fused = !(E.cfg.flags & 4);
         unsigned long long* krange = topk_range_reset(E.topk, E.s, fused, (E.cfg.flags & 8) != 0);
@@ -1131,11 +1137,12 @@ static void engine_step(Engine& E, sb_step_stats* out) {
 #define SB_EMIT_GRID 1536   // = resident blocks (24 KB LDS: 6 per CU): no partial second round of blocks
 #endif
         const unsigned egf = grid_cap(n, 256, SB_EMIT_GRID);   // fewer blocks: one histogram flush per block
+        const bool desc32 = desc_payload_ok(n);   // 4-byte descriptors, carried by the top-k (finish_turn)
         switch (E.cfg.heuristic) {
 #define EMIT(H)                                                                                                   \
     hipLaunchKernelGGL((k_emit_w<H, false>), dim3(egf), dim3(256), 0, E.s, E.d_tables, cur.lo, cur.hi, n, E.cand.p, \
                        E.lost.p, E.off.p, E.nlo.p, E.nhi.p, E.npar.p, E.skey.p, E.noise.ring.p, E.noise.ring_mask, \
-                       rbase, 0u, E.d_small + 1, krange, fh, fb);                                                 \
+                       rbase, 0u, E.d_small + 1, krange, fh, fb, (int)desc32);                                    \
     break;
             case 1: EMIT(1)
             case 2: EMIT(2)
@@ -1168,11 +1175,7 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
     // ---- prune + next beam
     int64_t m = nu;
     uint32_t* idx = nullptr;
-#ifndef SB_TOPK_DESC
-#define SB_TOPK_DESC 1   // the top-k carries each kept survivor's descriptor (rank << 8 | dsc) instead of its index
-#endif
-    // descriptors fit the 32-bit payload while parent ranks < 2^24
-    const bool desc_pay = SB_TOPK_DESC && desc && heur && !host_scores && n < ((int64_t)1 << 24);
+    const bool desc_pay = desc && heur && !host_scores && desc_payload_ok(n);
     if (heur) {
         E.kidx.ensure(std::min<int64_t>(nu, E.cfg.beam_width));
         if (host_scores) {   // f64 scores -> order-preserving u64 keys (a NaN sets error bit 16)
@@ -1182,7 +1185,8 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
                                  E.d_small + 1, /*fused=*/false);
         } else {
             m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true,
-                                 E.d_small + 1, /*fused=*/!(E.cfg.flags & 4), desc_pay ? E.nlo.p : nullptr);
+                                 E.d_small + 1, /*fused=*/!(E.cfg.flags & 4),
+                                 desc_pay ? reinterpret_cast<const uint32_t*>(E.nlo.p) : nullptr);
         }
         idx = E.kidx.p;
     }

@@ -114,11 +114,11 @@ struct TopkScratch {
 // sort's look-back wait hit its spin bound (reported by check_err_word; never expected).
 // fused: the producer also added every key to the first-pass histogram (topk_fused_hist/_base; keys
 // are IEEE images of positive doubles), which replaces the generic first select pass when usable.
-// payload: out_idx receives (uint32_t)payload[i] of the kept positions i instead of i (the descriptors
-// of next_queue: the gather then needs no random read of them).
+// payload: out_idx receives payload[i] of the kept positions i instead of i (next_queue's 4-byte
+// descriptors: the gather then reads none of them at a random line).
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
                          hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false,
-                         const uint64_t* payload = nullptr);
+                         const uint32_t* payload = nullptr);
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false);
 unsigned long long* topk_fused_hist(TopkScratch& s);
 const uint64_t* topk_fused_base(TopkScratch& s);

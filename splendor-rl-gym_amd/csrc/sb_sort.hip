@@ -403,7 +403,7 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ gi, const uint64_t* __restrict__ gbase,
                                                     uint64_t* __restrict__ ek, uint32_t* __restrict__ ei,
                                                     const uint64_t* __restrict__ ebase, const uint64_t* __restrict__ limit,
-                                                    const uint64_t* __restrict__ pay) {
+                                                    const uint32_t* __restrict__ pay) {
     constexpr int NW = TK_NT / 64;
     __shared__ uint32_t cnt[TK_IPT * NW];   // (round, wave): above | equal << 16, then exclusive offsets
     const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
@@ -451,12 +451,12 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
                 if ((fg >> r) & 1) {
                     const uint64_t o = og + (c & 0xFFFFu) + __popcll(bg & lt);
                     gk[o] = kk[r];
-                    gi[o] = idx ? idx[i] : (pay ? (uint32_t)pay[i] : (uint32_t)i);
+                    gi[o] = idx ? idx[i] : (pay ? pay[i] : (uint32_t)i);
                 } else if ((fe >> r) & 1) {
                     const uint64_t re = oe + (c >> 16) + __popcll(be & lt);
                     if (re < lim) {
                         ek[eb + re] = kk[r];
-                        ei[eb + re] = idx ? idx[i] : (pay ? (uint32_t)pay[i] : (uint32_t)i);
+                        ei[eb + re] = idx ? idx[i] : (pay ? pay[i] : (uint32_t)i);
                     }
                 }
             }
@@ -465,9 +465,9 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
     }
 }
 
-__global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64_t n, const uint64_t* pay) {
+__global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64_t n, const uint32_t* pay) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        v[i] = pay ? (uint32_t)pay[i] : (uint32_t)i;
+        v[i] = pay ? pay[i] : (uint32_t)i;
         okeys[i] = keys[i];
     }
 }
@@ -981,7 +981,7 @@ unsigned long long* topk_fused_hist(TopkScratch& s) { return (unsigned long long
 const uint64_t* topk_fused_base(TopkScratch& s) { return s.small.p + ST_FBASE; }
 
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready, uint32_t* err, bool fused, const uint64_t* payload) {
+                         hipStream_t st, bool range_ready, uint32_t* err, bool fused, const uint32_t* payload) {
     if (n <= 0 || keep <= 0) return 0;
     const int64_t m = n < keep ? n : keep;
     s.k0.ensure(m);
@@ -1039,7 +1039,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
                            (int)ST_E2, 1);
         hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
                            s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
-                           stv + ST_NEED, (const uint64_t*)nullptr);
+                           stv + ST_NEED, (const uint32_t*)nullptr);
     } else {
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m, payload);
     }
