@@ -74,15 +74,15 @@ def main(args):
     first, length, turns = probe_window(make, lambda s: s.step(), close, W)
     win = Window(make, lambda s: s.step(), lambda s: torch.cuda.synchronize(), close, first, length,
                  look=None if args.lookahead_edges else (lambda s, on: setattr(s, 'lookahead', on)))
-    def sync_end(_s):   # the timed turns' work (the engine runs on torch's stream); noise rounds ahead not waited for
+    def sync_engine(_s):   # the timed turns' work (the engine runs on torch's stream); noise rounds ahead not waited for
         torch.cuda.current_stream().synchronize()
-        dist.barrier()
 
-    per, el = timed_steps(win, args.steps, args.warmup, sync_all,
-                          sync_end=None if args.sync_all_streams else sync_end)
+    per, el, el_eng, segs = timed_steps(win, args.steps, args.warmup, sync_all, sync_engine=sync_engine,
+                                        engine_end=args.engine_stream_end)
     win.close()
     comm = Comm(torch.device('cuda', dev))
     el_max = float(comm.allreduce(np.array([int(el * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9
+    el_eng_max = float(comm.allreduce(np.array([int(el_eng * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9
     parents = sum(p['n_parents'] for p in per)
     raw = sum(p['n_raw'] for p in per)
     uniq = sum(p['n_unique'] for p in per)
@@ -107,8 +107,10 @@ def main(args):
                        'timed_turns': [first, first + length - 1], 'moves': turns,
                        'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
                                             if args.lookahead_edges else 'exactly the timed turns\' own'),
-                       'segment_end': ('every stream' if args.sync_all_streams else
-                                       'the engine stream (noise rounds for later turns not waited for)')},
+                       'segment_end': ('the engine stream (legacy: noise rounds for later turns not waited for)'
+                                       if args.engine_stream_end else 'every stream + barrier'),
+                       'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh solves)'},
+            'value_engine_stream_end': round(parents / el_eng_max, 1),
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
@@ -119,8 +121,8 @@ def main(args):
             out['roofline']['traffic'] = sh['hbm_bytes_per_launch']
             out['roofline']['traffic_kernel'] = sh['kernel']
             out['roofline']['traffic_source'] = sh['source']
-        if not args.no_cpu_baseline:   # after the timed region; the other ranks wait at the barrier below
-            out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, min(args.cpu_budget_s, 20.0))
+        if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only, after the timed region
+            out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, first)
         sys.stdout.flush()
         os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)

@@ -155,6 +155,9 @@ int sb_visited_capacity(sb_engine* e, uint64_t* capacity, int32_t* rebuilds);
 void sb_destroy(sb_engine* e);
 const char* sb_last_error(void);
 int sb_version(void);
+/* Identity of the sources the library was built from (sha256 prefix over csrc/ + this header, passed
+ * by the build); the ctypes loader compares it with the tree and refuses a stale library. */
+const char* sb_build_id(void);
 
 /* ---- kernel-level entry points for parity tests (same device code as sb_step) ---- */
 /* Ordered successors of n parents, stride 192 per parent: out_count[i] children for parent i. */

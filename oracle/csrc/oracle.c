@@ -25,11 +25,14 @@
  *   hi = cards 64..89 (bits 0..25) | gems g_i at bits 26+3i (3 bits each) | pts bits 41..48
  *        | saved bits 49..63
  */
+#include <fcntl.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #define NCARDS 90
 #define NCOL 5
@@ -129,7 +132,8 @@ static inline st_t st_make(uint64_t lo, uint64_t cards_hi, const int g[NCOL], in
 
 static void st_bonus(st_t s, int b[NCOL]) {
     for (int i = 0; i < NCOL; i++) b[i] = 0;
-    for (int c = 0; c < NCARDS; c++) if (st_has(s, c)) b[DECK[c].color]++;
+    for (uint64_t m = s.lo; m; m &= m - 1) b[DECK[__builtin_ctzll(m)].color]++;
+    for (uint64_t m = s.hi & ((1ull << 26) - 1); m; m &= m - 1) b[DECK[64 + __builtin_ctzll(m)].color]++;
 }
 
 /* ------------------------------------------------------------------ CPython tuple hash */
@@ -143,9 +147,10 @@ static inline uint64_t th_fin(uint64_t acc, uint64_t len) {
     return acc == ~0ull ? 1546275796ull : acc;
 }
 
-static uint64_t hash_cards(st_t s) {
+static uint64_t hash_cards(st_t s) {   /* sorted card tuple: ascending bit order */
     uint64_t acc = XXP5; int n = 0;
-    for (int c = 0; c < NCARDS; c++) if (st_has(s, c)) { acc = th_step(acc, (uint64_t)c); n++; }
+    for (uint64_t m = s.lo; m; m &= m - 1, n++) acc = th_step(acc, (uint64_t)__builtin_ctzll(m));
+    for (uint64_t m = s.hi & ((1ull << 26) - 1); m; m &= m - 1, n++) acc = th_step(acc, (uint64_t)(64 + __builtin_ctzll(m)));
     return th_fin(acc, (uint64_t)n);
 }
 static uint64_t hash_gems(const int g[NCOL]) {
@@ -284,20 +289,32 @@ int oc_mt_words(const uint32_t* state625, uint32_t* out, int n) {
 }
 
 /* ------------------------------------------------------------------ visited set (u64 keys) */
-typedef struct { uint64_t* slot; uint64_t mask; uint64_t n; } hset_t;
+/* The trail's capacity never changes a result (membership only).  Large tables (C5: about 2G keys)
+ * are reserved up front on 2 MB pages and may fill to 90% instead of doubling past the host's RAM. */
+typedef struct { uint64_t* slot; uint64_t mask; uint64_t n; uint64_t soft_cap; } hset_t;
 static inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33; return x;
 }
+static void* big_alloc(size_t bytes) {
+    void* p = NULL;
+    if (bytes >= (1u << 21)) {
+        if (posix_memalign(&p, 1u << 21, bytes)) return NULL;
+        madvise(p, bytes, MADV_HUGEPAGE);
+        return p;
+    }
+    return malloc(bytes);
+}
 static int hs_init(hset_t* h, uint64_t cap_pow2) {
-    h->slot = (uint64_t*)malloc(cap_pow2 * 8);
+    h->slot = (uint64_t*)big_alloc(cap_pow2 * 8);
     if (!h->slot) return -1;
     memset(h->slot, 0xFF, cap_pow2 * 8);
     h->mask = cap_pow2 - 1; h->n = 0;
     return 0;
 }
-static int hs_grow(hset_t* h) {
+static int hs_rehash(hset_t* h, uint64_t slots) {
     hset_t g;
-    if (hs_init(&g, (h->mask + 1) * 2)) return -1;
+    if (hs_init(&g, slots)) return -1;
+    g.soft_cap = h->soft_cap;
     for (uint64_t i = 0; i <= h->mask; i++) {
         uint64_t k = h->slot[i];
         if (k == ~0ull) continue;
@@ -308,9 +325,14 @@ static int hs_grow(hset_t* h) {
     free(h->slot); *h = g;
     return 0;
 }
+static inline int hs_full(const hset_t* h) {
+    uint64_t slots = h->mask + 1;
+    if (h->soft_cap && slots >= h->soft_cap) return (h->n + 1) * 10 > slots * 9;
+    return (h->n + 1) * 2 > slots;
+}
 /* returns 1 if inserted (new), 0 if present; key ~0 never occurs (tuple hash maps -1 away) */
 static int hs_insert(hset_t* h, uint64_t k) {
-    if ((h->n + 1) * 2 > h->mask + 1) hs_grow(h);
+    if (hs_full(h) && hs_rehash(h, (h->mask + 1) * 2)) { fprintf(stderr, "oracle: visited set OOM\n"); abort(); }
     uint64_t j = mix64(k) & h->mask;
     for (;;) {
         uint64_t v = h->slot[j];
@@ -322,9 +344,10 @@ static int hs_insert(hset_t* h, uint64_t k) {
 
 /* ------------------------------------------------------------------ beam solve handle */
 typedef struct {
-    st_t* st;        /* states of this turn, queue order */
+    st_t* st;        /* states of this turn, queue order (NULL once spilled to the spill file) */
     uint32_t* par;   /* parent rank in previous turn */
     int64_t n;
+    int64_t spill_off;
 } turn_t;
 
 typedef struct {
@@ -338,6 +361,8 @@ typedef struct {
     mt_t mt;
     hset_t visited;
     turn_t* turns; int nturns, capturns;
+    int spill_fd;    /* >= 0: earlier turns' states live in this (unlinked) file */
+    int64_t spill_end;
 } oc_handle;
 
 typedef struct {
@@ -356,7 +381,50 @@ static void push_turn(oc_handle* h, st_t* st, uint32_t* par, int64_t n) {
         h->turns = (turn_t*)realloc(h->turns, sizeof(turn_t) * h->capturns);
     }
     h->turns[h->nturns].st = st; h->turns[h->nturns].par = par; h->turns[h->nturns].n = n;
+    h->turns[h->nturns].spill_off = -1;
     h->nturns++;
+}
+
+/* Memory knobs for the C5-width golden (W=32M; results do not depend on them):
+ * reserve the visited set at 2^log2_slots (it then fills to 90% before doubling) and keep every
+ * turn but the newest in a spill file under `dir` instead of RAM. */
+int oc_set_lean(oc_handle* h, int log2_slots, const char* dir) {
+    if (log2_slots > 0) {
+        h->visited.soft_cap = 1ull << log2_slots;
+        if (h->visited.mask + 1 < h->visited.soft_cap && hs_rehash(&h->visited, h->visited.soft_cap)) return -1;
+    }
+    if (dir && dir[0]) {
+        char path[4096];
+        snprintf(path, sizeof path, "%s/oracle_spill_XXXXXX", dir);
+        int fd = mkstemp(path);
+        if (fd < 0) return -2;
+        unlink(path);
+        h->spill_fd = fd;
+    }
+    return 0;
+}
+
+static int spill_turn(oc_handle* h, int t) {
+    turn_t* tt = &h->turns[t];
+    if (h->spill_fd < 0 || !tt->st) return 0;
+    const char* p = (const char*)tt->st;
+    int64_t left = tt->n * (int64_t)sizeof(st_t), off = h->spill_end;
+    while (left > 0) {
+        ssize_t w = pwrite(h->spill_fd, p, left > (1 << 30) ? (1 << 30) : left, off);
+        if (w <= 0) return -1;
+        p += w; off += w; left -= w;
+    }
+    tt->spill_off = h->spill_end; h->spill_end = off;
+    free(tt->st); tt->st = NULL;
+    return 0;
+}
+
+static st_t turn_state(oc_handle* h, int t, int64_t r) {
+    turn_t* tt = &h->turns[t];
+    if (tt->st) return tt->st[r];
+    st_t s = {0, 0};
+    if (pread(h->spill_fd, &s, sizeof s, tt->spill_off + r * (int64_t)sizeof(st_t)) != (ssize_t)sizeof s) abort();
+    return s;
 }
 
 oc_handle* oc_create(int goal, int use_heuristic, int heuristic, int64_t beam_width,
@@ -364,6 +432,7 @@ oc_handle* oc_create(int goal, int use_heuristic, int heuristic, int64_t beam_wi
     if (!DECK_READY) return NULL;
     oc_handle* h = (oc_handle*)calloc(1, sizeof(oc_handle));
     h->goal = goal; h->use_heuristic = use_heuristic; h->heuristic = heuristic; h->beam_width = beam_width;
+    h->spill_fd = -1;
     memcpy(h->mt.mt, mt_state625, 624 * 4); h->mt.idx = (int)mt_state625[624]; h->mt.words = 0;
     hs_init(&h->visited, 1u << 20);
     st_t* root = (st_t*)malloc(sizeof(st_t)); root->lo = root_lo; root->hi = root_hi;
@@ -377,6 +446,7 @@ oc_handle* oc_create(int goal, int use_heuristic, int heuristic, int64_t beam_wi
 void oc_destroy(oc_handle* h) {
     if (!h) return;
     for (int t = 0; t < h->nturns; t++) { free(h->turns[t].st); free(h->turns[t].par); }
+    if (h->spill_fd >= 0) close(h->spill_fd);
     free(h->turns); free(h->visited.slot); free(h);
 }
 
@@ -402,11 +472,40 @@ static void sort_desc_stable(const uint64_t* key, uint32_t* idx, int64_t n) {
     free(tmp); free(kk); free(kt);
 }
 
+/* Stable top-W of `key` (descending, ties in index order) as ascending candidate indices: an MSB
+ * radix select (16-bit digits) finds the W-th largest value T; every key > T is kept, and the first
+ * W - #(> T) keys equal to T in index order.  Returns the count (min(n, W)).  Same set and order as
+ * a full stable sort followed by [:W] (src/solver.py:452-456), with sort scratch for W entries only. */
+static int64_t select_top(const uint64_t* key, int64_t n, int64_t W, uint32_t* out) {
+    if (n <= W) { for (int64_t i = 0; i < n; i++) out[i] = (uint32_t)i; return n; }
+    uint64_t prefix = 0, pmask = 0;
+    int64_t need = W;
+    int64_t* hist = (int64_t*)malloc(sizeof(int64_t) * 65536);
+    for (int sh = 48; sh >= 0; sh -= 16) {
+        memset(hist, 0, sizeof(int64_t) * 65536);
+        for (int64_t i = 0; i < n; i++)
+            if ((key[i] & pmask) == prefix) hist[(key[i] >> sh) & 0xFFFF]++;
+        int64_t above = 0;
+        int d = 65535;
+        for (; d > 0 && above + hist[d] < need; d--) above += hist[d];
+        need -= above;
+        prefix |= (uint64_t)d << sh; pmask |= 0xFFFFull << sh;
+    }
+    free(hist);
+    int64_t m = 0;
+    for (int64_t i = 0; i < n; i++) {
+        if (key[i] > prefix) out[m++] = (uint32_t)i;
+        else if (key[i] == prefix && need > 0) { out[m++] = (uint32_t)i; need--; }
+    }
+    return m;
+}
+
 /* One beam step (src/solver.py:434-457). */
 int oc_step(oc_handle* h, oc_stats* out) {
     memset(out, 0, sizeof *out);
     if (h->done) { out->done = 1; out->winner_rank = h->winner_rank; return 0; }
-    turn_t* cur = &h->turns[h->nturns - 1];
+    int tcur = h->nturns - 1;
+    turn_t* cur = &h->turns[tcur];
     out->n_parents = cur->n;
     /* goal check + max_pts records in queue order (:438-445) */
     for (int64_t r = 0; r < cur->n; r++) {
@@ -421,22 +520,37 @@ int oc_step(oc_handle* h, oc_stats* out) {
             return 0;
         }
     }
-    /* expansion + trail dedup (:446-450) */
+    /* expansion + trail dedup (:446-450).  Children of PB parents are generated and their slots
+     * prefetched together, then inserted one by one in (parent rank, ordinal) order. */
+    enum { PB = 16 };
     int64_t cap = cur->n * 32 + 256, nq = 0, nraw = 0;
-    st_t* nxt = (st_t*)malloc(sizeof(st_t) * cap);
-    uint32_t* npar = (uint32_t*)malloc(sizeof(uint32_t) * cap);
-    st_t kids[256];
-    for (int64_t r = 0; r < cur->n; r++) {
-        int nk = successors(cur->st[r], kids);
-        nraw += nk;
-        for (int k = 0; k < nk; k++) {
-            if (!hs_insert(&h->visited, oc_state_key(kids[k].lo, kids[k].hi))) continue;
-            if (nq == cap) {
-                cap *= 2;
-                nxt = (st_t*)realloc(nxt, sizeof(st_t) * cap);
-                npar = (uint32_t*)realloc(npar, sizeof(uint32_t) * cap);
+    st_t* nxt = (st_t*)big_alloc(sizeof(st_t) * cap);
+    uint32_t* npar = (uint32_t*)big_alloc(sizeof(uint32_t) * cap);
+    static __thread st_t kids[PB * 256];
+    static __thread uint64_t kkey[PB * 256];
+    static __thread int kcnt[PB];
+    for (int64_t r0 = 0; r0 < cur->n; r0 += PB) {
+        int np = cur->n - r0 < PB ? (int)(cur->n - r0) : PB, tot = 0;
+        for (int j = 0; j < np; j++) {
+            int nk = successors(cur->st[r0 + j], kids + tot);
+            for (int k = 0; k < nk; k++) {
+                uint64_t key = oc_state_key(kids[tot + k].lo, kids[tot + k].hi);
+                kkey[tot + k] = key;
+                __builtin_prefetch(&h->visited.slot[mix64(key) & h->visited.mask]);
             }
-            nxt[nq] = kids[k]; npar[nq] = (uint32_t)r; nq++;
+            kcnt[j] = nk; tot += nk;
+        }
+        nraw += tot;
+        for (int j = 0, e = 0; j < np; j++) {
+            for (int k = 0; k < kcnt[j]; k++, e++) {
+                if (!hs_insert(&h->visited, kkey[e])) continue;
+                if (nq == cap) {
+                    cap *= 2;
+                    nxt = (st_t*)realloc(nxt, sizeof(st_t) * cap);
+                    npar = (uint32_t*)realloc(npar, sizeof(uint32_t) * cap);
+                }
+                nxt[nq] = kids[e]; npar[nq] = (uint32_t)(r0 + j); nq++;
+            }
         }
     }
     out->n_raw = nraw; out->n_unique = nq;
@@ -447,24 +561,30 @@ int oc_step(oc_handle* h, oc_stats* out) {
         return 0;
     }
     if (h->use_heuristic) {  /* sorted(next_queue, key=heuristic, reverse=True)[:beam_width] (:452-456) */
-        uint64_t* key = (uint64_t*)malloc(sizeof(uint64_t) * nq);
-        uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * nq);
+        uint64_t* key = (uint64_t*)big_alloc(sizeof(uint64_t) * nq);
         for (int64_t i = 0; i < nq; i++) {
             double sc = score_base(nxt[i], h->heuristic, (double)mt_randint100(&h->mt) * 0.01);
             memcpy(&key[i], &sc, 8);   /* scores are > 0: IEEE bits order == numeric order */
         }
-        sort_desc_stable(key, idx, nq);
-        int64_t nk = nq < h->beam_width ? nq : h->beam_width;
+        int64_t W = nq < h->beam_width ? nq : h->beam_width;
+        uint32_t* cand = (uint32_t*)malloc(sizeof(uint32_t) * (W ? W : 1));
+        int64_t nk = select_top(key, nq, W, cand);
+        uint64_t* ckey = (uint64_t*)malloc(sizeof(uint64_t) * (nk ? nk : 1));
+        uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (nk ? nk : 1));
+        for (int64_t i = 0; i < nk; i++) ckey[i] = key[cand[i]];
+        free(key);
+        sort_desc_stable(ckey, idx, nk);
         st_t* ks = (st_t*)malloc(sizeof(st_t) * (nk ? nk : 1));
         uint32_t* kp = (uint32_t*)malloc(sizeof(uint32_t) * (nk ? nk : 1));
-        for (int64_t i = 0; i < nk; i++) { ks[i] = nxt[idx[i]]; kp[i] = npar[idx[i]]; }
-        free(key); free(idx); free(nxt); free(npar);
+        for (int64_t i = 0; i < nk; i++) { ks[i] = nxt[cand[idx[i]]]; kp[i] = npar[cand[idx[i]]]; }
+        free(ckey); free(idx); free(cand); free(nxt); free(npar);
         push_turn(h, ks, kp, nk);
         out->n_kept = nk;
     } else {
         push_turn(h, nxt, npar, nq);
         out->n_kept = nq;
     }
+    if (spill_turn(h, tcur)) return -3;
     h->turn++;
     out->mt_words = h->mt.words;
     return 0;
@@ -477,13 +597,24 @@ int oc_read_turn(oc_handle* h, int t, int64_t start, int64_t n, uint64_t* lo, ui
     if (t < 0 || t >= h->nturns) return -1;
     turn_t* tt = &h->turns[t];
     if (start < 0 || start + n > tt->n) return -2;
+    st_t* blk = tt->st ? tt->st + start : NULL;
+    if (!blk) {   /* spilled turn: one read of the range */
+        blk = (st_t*)malloc(sizeof(st_t) * (n ? n : 1));
+        const int64_t bytes = n * (int64_t)sizeof(st_t);
+        for (int64_t done = 0; done < bytes;) {
+            ssize_t r = pread(h->spill_fd, (char*)blk + done, bytes - done, tt->spill_off + start * (int64_t)sizeof(st_t) + done);
+            if (r <= 0) { free(blk); return -3; }
+            done += r;
+        }
+    }
     for (int64_t i = 0; i < n; i++) {
-        st_t s = tt->st[start + i];
+        st_t s = blk[i];
         if (lo) lo[i] = s.lo;
         if (hi) hi[i] = s.hi;
         if (par) par[i] = tt->par[start + i];
         if (key) key[i] = oc_state_key(s.lo, s.hi);
     }
+    if (blk != (tt->st ? tt->st + start : NULL)) free(blk);
     return 0;
 }
 
@@ -495,7 +626,8 @@ int oc_path(oc_handle* h, uint64_t* lo, uint64_t* hi, int cap) {
     int len = t + 1;
     if (len > cap) return -2;
     for (; t >= 0; t--) {
-        lo[t] = h->turns[t].st[r].lo; hi[t] = h->turns[t].st[r].hi;
+        st_t s = turn_state(h, t, r);
+        lo[t] = s.lo; hi[t] = s.hi;
         r = (int64_t)h->turns[t].par[r];
     }
     return len;
@@ -506,6 +638,13 @@ int oc_get_mt_state(oc_handle* h, uint32_t* out625) {
     return 0;
 }
 uint64_t oc_visited_size(oc_handle* h) { return h->visited.n; }
+/* the trail's keys (any order), at most cap; returns the count written */
+int64_t oc_visited_keys(oc_handle* h, uint64_t* out, int64_t cap) {
+    int64_t m = 0;
+    for (uint64_t i = 0; i <= h->visited.mask && m < cap; i++)
+        if (h->visited.slot[i] != ~0ull) out[m++] = h->visited.slot[i];
+    return m;
+}
 
 /* ====================================================================================== */
 /* Realistic multi-player mode (src/solver.py:25-200, 471-860): TEST INFRASTRUCTURE ONLY.

@@ -1273,6 +1273,11 @@ static int guarded(F&& f) {
 extern "C" {
 
 int sb_version(void) { return 1; }
+#ifndef SB_BUILD_ID
+#define SB_BUILD_ID "unknown"
+#endif
+// sha256 of the sources this library was compiled from (_lib.source_hash): the loader refuses a stale build
+const char* sb_build_id(void) { return SB_BUILD_ID; }
 const char* sb_last_error(void) { return g_err.c_str(); }
 
 int sb_init_tables(const int32_t* deck_rows, const double* pow_tables, const double* noise) {

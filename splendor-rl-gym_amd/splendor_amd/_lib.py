@@ -7,6 +7,7 @@ no CPU fallback (the CPU restatement under ``oracle/`` is test infrastructure).
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 import subprocess
 
@@ -31,7 +32,7 @@ SB_HEUR_HOST = 15   # a Python HEURISTICS callable scores next_queue on the host
 POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
 EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_read_next', 'sb_prune', 'sb_turn_times', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
-            'sb_get_mt_state', 'sb_sync', 'sb_set_lookahead', 'sb_sync_engine', 'sb_visited_size', 'sb_visited_capacity', 'sb_destroy', 'sb_last_error', 'sb_version',
+            'sb_get_mt_state', 'sb_sync', 'sb_set_lookahead', 'sb_sync_engine', 'sb_visited_size', 'sb_visited_capacity', 'sb_destroy', 'sb_last_error', 'sb_version', 'sb_build_id',
             'sb_debug_successors', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk',
             'sbd_goal_table', 'sbd_expand_launch', 'sbd_expand_counts', 'sbd_pack', 'sbd_owner_begin', 'sbd_owner_claim', 'sbd_owner_finish', 'sbd_pack_bits', 'sbd_unpack_bits', 'sbd_apply', 'sbd_apply_finish', 'sbd_emit',
             'sbd_key_range', 'sbd_sel_begin', 'sbd_sel_hist', 'sbd_sel_pick', 'sbd_sel_compact', 'sbd_sel_eq', 'sbd_set_stream', 'sbd_noise_info', 'sbd_noise_chunk', 'sbd_noise_sync', 'sbd_noise_pack', 'sbd_noise_fill', 'sbd_partition', 'sbd_partition_bfs', 'sbd_pack_kept', 'sbd_receive', 'sbd_mark_done',
@@ -65,25 +66,47 @@ class SbStepStats(C.Structure):
         return d
 
 
+HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), 'include', 'splendor_beam.h')
+
+
+def source_hash() -> str | None:
+    """sha256 prefix over the engine's sources (csrc/*.hip, *.inc, *.h and the C-ABI header), or None
+    when the sources are not present (an installed library without its tree)."""
+    if not os.path.isdir(CSRC):
+        return None
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith(('.hip', '.inc', '.h')))
+    for f in files:
+        h.update(f.encode() + b'\0')
+        with open(os.path.join(CSRC, f), 'rb') as fh:
+            h.update(fh.read())
+    if os.path.exists(HEADER):
+        with open(HEADER, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(verbose: bool = False, out: str | None = None, defines: tuple = ()) -> str:
     """Compile the HIP sources for gfx950 into the in-tree shared library (or `out`, with -D `defines`)."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     out = out or LIB_PATH
     cmd = ['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off',
-           '-Wall', '-Wno-unused-function', *[f'-D{d}' for d in defines], *srcs, '-o', out]
+           '-Wall', '-Wno-unused-function', f'-DSB_BUILD_ID="{source_hash()}"', *[f'-D{d}' for d in defines], *srcs,
+           '-o', out]
     if verbose:
         print(' '.join(cmd))
     subprocess.run(cmd, check=True)
     return out
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] if os.path.isdir(CSRC) else []
-    deps.append(os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), 'include', 'splendor_beam.h'))
-    return any(os.path.exists(p) and os.path.getmtime(p) > t for p in deps)
+def check_fresh(L, path: str) -> None:
+    """Refuse a library built from other sources than the tree's (a run that skipped build())."""
+    want = source_hash()
+    L.sb_build_id.restype = C.c_char_p
+    have = L.sb_build_id().decode()
+    if want is not None and have != want:
+        raise ImportError(f'{path} is stale: built from sources {have}, tree is {want}; '
+                          'rebuild it (python __graft_entry__.py, or splendor_amd._lib.build())')
 
 
 _lib = None
@@ -97,6 +120,7 @@ def lib():
         if not os.path.exists(LOAD_PATH):
             raise ImportError(f'{LOAD_PATH} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)')
         L = C.CDLL(LOAD_PATH)
+        check_fresh(L, LOAD_PATH)
         u64p = np.ctypeslib.ndpointer(np.uint64, flags='C')
         u32p = np.ctypeslib.ndpointer(np.uint32, flags='C')
         i32p = np.ctypeslib.ndpointer(np.int32, flags='C')

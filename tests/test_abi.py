@@ -60,3 +60,21 @@ def test_init_tables_validates_deck():
     assert rc == _lib.SB_ERR_ARG
     _lib._tables_ready = False
     _lib.ensure_tables()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library built from other sources than the tree's is refused: the build
+    stamps sb_build_id with the sources' sha256; editing any source changes the tree's hash."""
+    import shutil
+    L = _lib.lib()
+    _lib.check_fresh(L, _lib.LIB_PATH)          # the in-tree build matches its sources
+    csrc = tmp_path / 'csrc'
+    shutil.copytree(_lib.CSRC, csrc)
+    monkeypatch.setattr(_lib, 'CSRC', str(csrc))
+    assert _lib.source_hash() == L.sb_build_id().decode()
+    with open(csrc / 'sb_engine.hip', 'a') as f:  # "touch" with an edit
+        f.write('\n// edited\n')
+    assert _lib.source_hash() != L.sb_build_id().decode()
+    import pytest
+    with pytest.raises(ImportError, match='stale'):
+        _lib.check_fresh(L, _lib.LIB_PATH)
