@@ -280,9 +280,44 @@ def run_single(args):
     return per, elapsed, el_eng, segs, (first, length, turns, win.engines)
 
 
+def rexpand_bytes(n_parents, n_raw, n_unique):
+    """Algorithmic bytes of k_rexpand per launch: the parent's 12-word state (96 B) and its
+    24 B of candidate / lost masks; per raw child a 16 B visited-entry probe; per new key an 8 B tag CAS
+    and an 8 B key store."""
+    return 120 * n_parents + 16 * n_raw + 16 * n_unique
+
+
+def cpu_baseline_realistic(width, seed, first_turn):
+    """The realistic C oracle (oracle/csrc/oracle.c, ort_*), 1 thread, on the first timed turn of the same
+    seeded C4 trajectory (setup turns untimed)."""
+    import numpy as np
+    import oracle_c
+    from splendor_amd.engine_rt import device_tiers
+    from splendor_amd.realistic import GameConfig, MultiPlayerState, game_params, pack_state
+    cfg = GameConfig(num_players=2, target_points=15, gems_per_color=4, infinite_resources=False)
+    root = MultiPlayerState.newgame(config=cfg, shuffle_market=True, seed=seed)
+    tiers0 = device_tiers(root)
+    params, tiers = game_params(cfg, tiers0)
+    random.seed(seed)
+    o = oracle_c.OracleRealistic(params, tiers, beam_width=width, mt_state625=random.getstate()[1],
+                                 root_w=np.asarray(pack_state(root, tiers0)))
+    for _ in range(first_turn):
+        o.step()
+    t0 = time.perf_counter()
+    r = o.step()
+    dt = time.perf_counter() - t0
+    o.close()
+    return {'value': round(r['n_parents'] / dt, 1), 'unit': 'states/s', 'cores': 1, 'kind': 'port',
+            'sample': f'realistic C oracle (oracle/csrc/oracle.c ort_step), 1 thread: turn {first_turn} of the C4 '
+                      f'trajectory ({r["n_parents"]} parents), {dt:.2f} s; host cores available '
+                      f'{len(os.sched_getaffinity(0))}',
+            'python_reference_quoted': {'value': 3600, 'unit': 'states/s', 'cores': 1,
+                                        'source': 'the reference itself (MultiPlayerState.solve), SURVEY.md §8(a) '
+                                                  'a12, measured in the build container'}}
+
+
 def run_realistic(args):
     """Config C4: MultiPlayerState beam search, 2 players, goal 15, shuffled market (seed 0), W=1M."""
-    from splendor_amd import _lib
     from splendor_amd.engine_rt import RealisticEngine
     from splendor_amd.realistic import GameConfig, MultiPlayerState
     width = args.width if args.width != 4_000_000 else 1_000_000
@@ -291,24 +326,53 @@ def run_realistic(args):
     def make():
         root = MultiPlayerState.newgame(config=cfg, shuffle_market=True, seed=args.seed)
         random.seed(args.seed)
-        return RealisticEngine(root, beam_width=width, mt_state625=random.getstate()[1], device=0)
+        return RealisticEngine(root, beam_width=width, mt_state625=random.getstate()[1], device=0, timing=True)
 
+    from splendor_amd import _lib
     sync = lambda e: _lib.lib().sb_sync(e._h)
     first, length, turns = probe_window(make, lambda e: e.step(), lambda e: e.close(), width)
     win = Window(make, lambda e: e.step(), sync, lambda e: e.close(), first, length)
-    per, elapsed, _, segs = timed_steps(win, args.steps, args.warmup, sync)
+
+    def phases(eng, turn0, seg):
+        for i, p in enumerate(seg):
+            p.update(eng.turn_times(turn0 + i))
+
+    per, elapsed, _, segs = timed_steps(win, args.steps, args.warmup, sync, phases)
     win.close()
     parents = sum(p['n_parents'] for p in per)
+    raw = sum(p['n_raw'] for p in per)
+    uniq = sum(p['n_unique'] for p in per)
+    K = len(per)
+    ph = {k: round(sum(p[k] for p in per) / K, 3) for k in
+          ('ms_expand', 'ms_survive', 'ms_mt', 'ms_emit', 'ms_select', 'ms_gather', 'ms_total')}
+    byt = rexpand_bytes(parents / K, raw / K, uniq / K)
+    achieved = byt / (ph['ms_expand'] * 1e-3) / 1e9 if ph['ms_expand'] > 0 else 0.0
     out = {'metric': 'states expanded/sec per beam step, realistic 2-player goal 15 --shuffle, beam_width=1M',
-           'value': round(parents / elapsed, 1), 'unit': 'states/s', 'n_gpus': 1, 'steps': len(per),
-           'warmup': args.warmup, 'ms_per_step': round(elapsed / len(per) * 1e3, 3), 'higher_is_better': True,
+           'value': round(parents / elapsed, 1), 'unit': 'states/s', 'n_gpus': 1, 'steps': K,
+           'warmup': args.warmup, 'ms_per_step': round(elapsed / K * 1e3, 3), 'higher_is_better': True,
            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64+f64',
            'data': f'synthetic: seeded realistic solve trajectory (market shuffle seed {args.seed}, random.seed('
                    f'{args.seed})); timed: saturated turns {first}..{first + length - 1} of the {turns}-move game, '
                    f'replayed on {win.engines} seeded engines',
            'config': {'workload': f'realistic 2p goal_pts=15 --shuffle beam_width={width} (C4)', 'beam_width': width,
-                      'b_raw': round(sum(p['n_raw'] for p in per) / parents, 3),
-                      'b_uniq': round(sum(p['n_unique'] for p in per) / parents, 3)}}
+                      'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
+                      'segment_end': 'every stream', 'segments': segs,
+                      'warmup_engine': 'own (the timed steps start on fresh engines)'},
+           'phases_ms': ph,
+           'roofline': {'bound': 'hbm', 'kernel': 'k_rexpand', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+                        'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
+                        'algorithmic_bytes_per_launch': int(byt), 'launch_ms': ph['ms_expand'], 'traffic': None},
+           'cpu_baseline': None}
+    tr, tns, hit, src = pmc_traffic('k_rexpand<1>')
+    if tr is not None:
+        out['roofline']['traffic'] = int(tr)
+        out['roofline']['traffic_GBps'] = round(tr / (tns * 1e-9) / 1e9, 1)
+        if hit is not None:
+            out['roofline']['l2_hit_rate'] = round(hit, 4)
+        out['roofline']['traffic_source'] = f'{src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; ' \
+                                            f'hbm = (2*FETCH + WRITE) KiB, gfx950 correction)'
+    if not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline_realistic(width, args.seed, first)
     print(json.dumps(out))
 
 

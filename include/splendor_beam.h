@@ -173,6 +173,8 @@ int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const
                     const int32_t* k, int64_t n, double* out);
 /* Stable descending sort of n u64 keys: out_idx = permutation (ties keep input order), first `keep`. */
 int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx);
+/* sb_prune's host-scored prune alone: f64 scores (any sign or spacing) -> stable descending order. */
+int sb_debug_topk_scores(int32_t device, const double* scores, int64_t n, int64_t keep, uint32_t* out_idx);
 
 /* ---- sharded mode (cfg.world_size > 1 or flags bit 1): per-rank step primitives; the exchanges
  * between them are the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers

@@ -18,7 +18,7 @@ from collections import defaultdict
 # kernels launched once per step on the saturated path (k_expand: the last launches include the
 # pipelined expansion of the turn after the last timed one — one per step either way)
 PER_STEP = ['k_expand<false>', 'k_expand<true>', 'k_count_lm', 'k_emit_w<1, false>', 'k_tk_count', 'k_tk_write', 'k_os_hist', 'k_os_pass',
-            'k_gather_d', 'k_copy_idx']
+            'k_gather_d', 'k_copy_idx', 'k_rexpand<1>', 'k_remit<1>', 'k_rgather']
 
 
 def short(name):
@@ -31,6 +31,9 @@ def main():
     ap.add_argument('dir')
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--out', required=True)
+    ap.add_argument('--expand', default='k_expand',
+                    help='name prefix of the per-step expansion kernel that delimits the timed turns '
+                         '(k_rexpand for bench.py --realistic)')
     ap.add_argument('--edges', action='store_true',
                     help='the run used bench.py --lookahead-edges (round-2 accounting before session 4)')
     a = ap.parse_args()
@@ -50,7 +53,7 @@ def main():
         (default): the last S expansions are the timed turns' own and everything from the first of them
         on is timed.  --edges: the first timed turn's expansion was launched inside the step before it
         and the last timed step launched the next one: the window lies between those two starts."""
-        ex = [r for r in recs if r[0].startswith('k_expand')]
+        ex = [r for r in recs if r[0].startswith(a.expand)]
         if a.edges:
             t0, t1 = ex[-a.steps - 1][1], ex[-1][1]
         else:

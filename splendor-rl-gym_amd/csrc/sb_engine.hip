@@ -571,20 +571,9 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
         mhi[threadIdx.x] = T->colmask_hi[threadIdx.x];
     }
     __syncthreads();
-#ifndef SB_GATHER_PF
-#define SB_GATHER_PF 0   // A/B: prefetch the next descriptor of this thread while rebuilding the current one
-#endif
     const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t dnext = (SB_GATHER_PF && i0 < m) ? ndesc[idx[i0]] : 0;
-    for (int64_t i = i0; i < m; i += gstride) {
-        uint64_t dd;
-        if (SB_GATHER_PF) {
-            dd = dnext;
-            if (i + gstride < m) dnext = ndesc[idx[i + gstride]];
-        } else {
-            dd = desc_in_idx ? (uint64_t)idx[i] : ndesc[idx[i]];   // the top-k carried the descriptor itself
-        }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gstride) {
+        const uint64_t dd = desc_in_idx ? (uint64_t)idx[i] : ndesc[idx[i]];   // the top-k carried the descriptor itself
         const uint32_t r = (uint32_t)(dd >> 8);
         const int dsc = (int)(dd & 255);
         const uint64_t lo = plo[r], hi = phi[r];
@@ -1182,7 +1171,7 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
             SB_HIP(hipMemcpyAsync(E.skey.p, host_scores, (size_t)nu * 8, hipMemcpyHostToDevice, E.s));
             hipLaunchKernelGGL(k_order_keys, dim3(grid_cap(nu, 256, 8192)), dim3(256), 0, E.s, E.skey.p, nu, E.d_small + 1);
             m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/false,
-                                 E.d_small + 1, /*fused=*/false);
+                                 E.d_small + 1, /*fused=*/false, nullptr, /*full_key=*/true);
         } else {
             m = topk_stable_desc(E.skey.p, nu, E.cfg.beam_width, E.kidx.p, E.topk, E.s, /*range_ready=*/true,
                                  E.d_small + 1, /*fused=*/!(E.cfg.flags & 4),
@@ -1337,6 +1326,12 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         set_error("sb_create: bad beam_width or MT position");
         return SB_ERR_ARG;
     }
+    if ((cfg->world_size > 1 || (cfg->flags & 2)) && cfg->use_heuristic &&
+        (cfg->beam_width + std::max(1, (int)cfg->world_size) - 1) / std::max(1, (int)cfg->world_size) > (int64_t)SH_RANK_MASK + 1) {
+        // sharded: a rank's slice of the beam indexes its own claims' tags in 26 bits (SH_RANK_MASK)
+        set_error("sb_create: beam_width / world_size exceeds 2^26 parents per rank (sharded claim tags); use more ranks");
+        return SB_ERR_CAPACITY;
+    }
     sb_engine* h = new sb_engine();
     int rc = guarded([&]() {
         Engine& E = h->E;
@@ -1487,7 +1482,7 @@ int sb_prune(sb_engine* h, const double* scores, int64_t n, int64_t* n_kept) {
 }
 
 int sb_turn_times(sb_engine* h, int32_t turn, float* out7) {
-    if (!h || !out7 || h->E.mode != 0) return SB_ERR_ARG;
+    if (!h || !out7) return SB_ERR_ARG;
     return guarded([&]() {
         SB_HIP(hipSetDevice(h->E.dev));
         turn_times(h->E, turn, out7);
@@ -1772,6 +1767,40 @@ int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep,
         SB_HIP(hipFree(di));
         s.release();
         SB_HIP(hipStreamDestroy(st));
+        return SB_OK;
+    });
+}
+
+// the host-scored prune of sb_prune on its own: f64 scores -> order keys (k_order_keys) -> full-key top-k
+int sb_debug_topk_scores(int32_t device, const double* scores, int64_t n, int64_t keep, uint32_t* out_idx) {
+    if (!scores || !out_idx || n < 0 || keep < 0) return SB_ERR_ARG;
+    if (n == 0 || keep == 0) return SB_OK;
+    return guarded([&]() {
+        SB_HIP(hipSetDevice(device));
+        hipStream_t st;
+        SB_HIP(hipStreamCreate(&st));
+        uint64_t* dk;
+        uint32_t* di;
+        uint32_t* derr;
+        const int64_t m = std::min(n, keep);
+        SB_HIP(hipMalloc((void**)&dk, n * 8));
+        SB_HIP(hipMalloc((void**)&di, m * 4));
+        SB_HIP(hipMalloc((void**)&derr, 4));
+        SB_HIP(hipMemset(derr, 0, 4));
+        SB_HIP(hipMemcpy(dk, scores, n * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_order_keys, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, st, dk, n, derr);
+        TopkScratch s;
+        topk_stable_desc(dk, n, keep, di, s, st, false, derr, false, nullptr, /*full_key=*/true);
+        SB_HIP(hipStreamSynchronize(st));
+        uint32_t err = 0;
+        SB_HIP(hipMemcpy(&err, derr, 4, hipMemcpyDeviceToHost));
+        SB_HIP(hipMemcpy(out_idx, di, m * 4, hipMemcpyDeviceToHost));
+        SB_HIP(hipFree(dk));
+        SB_HIP(hipFree(di));
+        SB_HIP(hipFree(derr));
+        s.release();
+        SB_HIP(hipStreamDestroy(st));
+        if (err) throw HipError{hipErrorLaunchFailure, "sb_debug_topk_scores: device error word " + std::to_string(err)};
         return SB_OK;
     });
 }

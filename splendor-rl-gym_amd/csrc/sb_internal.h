@@ -116,9 +116,12 @@ struct TopkScratch {
 // are IEEE images of positive doubles), which replaces the generic first select pass when usable.
 // payload: out_idx receives payload[i] of the kept positions i instead of i (next_queue's 4-byte
 // descriptors: the gather then reads none of them at a random line).
+// full_key: sort on every varying key bit (up to 8 passes) instead of the top 40 + the exact fix-up, whose
+// runs of equal prefixes hold at most FX_LIST distinct keys (error bit 32 beyond): keys of arbitrary
+// distribution (host-scored heuristics, sb_prune) take this path.
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
                          hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false,
-                         const uint32_t* payload = nullptr);
+                         const uint32_t* payload = nullptr, bool full_key = false);
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false);
 unsigned long long* topk_fused_hist(TopkScratch& s);
 const uint64_t* topk_fused_base(TopkScratch& s);

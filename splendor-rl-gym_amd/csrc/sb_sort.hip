@@ -475,14 +475,14 @@ __global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64
 // bits that vary among the kept keys: [lowest kept, max]; lowest kept >= prefix << sh
 // The kept keys lie in [lo, max]: sorting key - lo (same order) needs only the bits of max - lo,
 // one digit fewer than the bits in which lo and max differ when the range crosses a power of two.
-__global__ void k_tk_sortsetup(uint64_t* st, int selected) {
+__global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) {
     uint64_t lo = st[ST_MIN];
     if (selected) lo = st[ST_SH] >= 64 ? 0ull : (st[ST_PREFIX] << st[ST_SH]);
     const uint64_t x = st[ST_MAX] - lo;
     const uint64_t topk = x ? 64 - (uint64_t)__clzll((long long)x) : 0;
     st[ST_SLO] = lo;
     st[ST_TOPK] = topk;
-    st[ST_SH32] = topk > OS_PREFIX_BITS ? topk - OS_PREFIX_BITS : 0;   // the sort orders the top varying bits
+    st[ST_SH32] = topk > (uint64_t)prefix_bits ? topk - prefix_bits : 0;   // the sort orders the top varying bits
     st[ST_FXN] = 0;
     st[ST_FXI] = 0;
 }
@@ -981,8 +981,10 @@ unsigned long long* topk_fused_hist(TopkScratch& s) { return (unsigned long long
 const uint64_t* topk_fused_base(TopkScratch& s) { return s.small.p + ST_FBASE; }
 
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
-                         hipStream_t st, bool range_ready, uint32_t* err, bool fused, const uint32_t* payload) {
+                         hipStream_t st, bool range_ready, uint32_t* err, bool fused, const uint32_t* payload,
+                         bool full_key) {
     if (n <= 0 || keep <= 0) return 0;
+    const int prefix_bits = full_key ? 64 : OS_PREFIX_BITS;
     const int64_t m = n < keep ? n : keep;
     s.k0.ensure(m);
     s.k1.ensure(m);
@@ -1044,9 +1046,9 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m, payload);
     }
 #ifdef SB_DBG_EMPTY   // diagnostic: extra empty launches (kernel boundary cost)
-    for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
+    for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
 #endif
-    hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected);
+    hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
     const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
     s.os.ensure(lb_words);
@@ -1061,7 +1063,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #define SB_OS_GRID 1u << 20   // blocks per pass at most (tiles beyond are taken by ticket)
 #endif
     const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
-    for (int p = 0; p < OS_MAX_PASSES; p++)
+    for (int p = 0; p < (prefix_bits + 7) / 8; p++)   // passes beyond the varying bits exit at once
         hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p);
     // exact order among keys that share their 32-bit prefix

@@ -1,7 +1,8 @@
 """Command line, flag-compatible with the reference's splendor_fastest_win.py:14-152.
 
 Same flags and output; adds --seed (random.seed before the solve, and the realistic market shuffle
-seed, for reproducible runs) and --device (GPU ordinal).  The solve runs on the MI355X engine.
+seed, for reproducible runs), --device (GPU ordinal) and --gpus N (the speedrun beam sharded over N GPUs,
+one worker process each: splendor_amd.multi).  The solve runs on the MI355X engine.
 """
 from __future__ import annotations
 
@@ -36,6 +37,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument('--seed', help='seed random (and the realistic market shuffle) for a reproducible run',
                    type=int, default=None)
     p.add_argument('--device', help='GPU ordinal (default 0)', type=int, default=0)
+    p.add_argument('--gpus', help='shard the speedrun beam over N GPUs, one process each (default 1)', type=int,
+                   default=1)
     return p
 
 
@@ -46,6 +49,10 @@ def cli(argv=None):
         parser.print_help()
         parser.exit()
     args = parser.parse_args(argv)
+    if args.gpus < 1:
+        parser.error('--gpus must be >= 1')
+    if args.gpus > 1 and args.realistic:
+        parser.error('--gpus > 1 shards the speedrun solve; --realistic runs on one GPU')
     if args.seed is not None:
         random.seed(args.seed)
     try:
@@ -84,7 +91,7 @@ def cli(argv=None):
             else:
                 solution = State.newgame().solve(goal_pts=args.goal_pts, use_heuristic=args.use_heuristic,
                                                  heuristic_name=args.heuristic, beam_width=args.beam_width,
-                                                 verbose=not args.quiet, device=args.device)
+                                                 verbose=not args.quiet, device=args.device, gpus=args.gpus)
                 if args.render:
                     render_solution(solution)
                 else:

@@ -35,14 +35,16 @@ def device_tiers(state):
 class RealisticEngine:
     """Stepwise realistic beam search on one MI355X."""
 
-    def __init__(self, root, *, beam_width: int, mt_state625, device: int = 0, visited_log2: int = 0, tiers=None):
+    def __init__(self, root, *, beam_width: int, mt_state625, device: int = 0, visited_log2: int = 0, tiers=None,
+                 timing: bool = False):
         L.ensure_tables()
         lib = _bind()
         self.config = root.config
         self.tiers0 = tiers if tiers is not None else device_tiers(root)
         self.params, self.tiers = game_params(root.config, self.tiers0)
         cfg = L.SbConfig(goal_pts=root.config.target_points, use_heuristic=1, heuristic=0, device=int(device),
-                         beam_width=int(beam_width), visited_log2=int(visited_log2), flags=0, world_size=1, rank=0)
+                         beam_width=int(beam_width), visited_log2=int(visited_log2), flags=1 if timing else 0,
+                         world_size=1, rank=0)
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
         L.check(lib.sbr_create(C.byref(cfg), self.params, self.tiers, st, pack_state(root, self.tiers0), C.byref(h)),
@@ -64,6 +66,14 @@ class RealisticEngine:
         d = s.as_dict()
         self.done = d['done']
         return d
+
+    def turn_times(self, t: int) -> dict:
+        """Device phase times (ms) of completed turn t (engine created with timing=True): expansion
+        (k_rexpand), survivor count + scan, emission, top-k, gather, total."""
+        out = np.zeros(7, np.float32)
+        L.check(L.lib().sb_turn_times(self._h, int(t), out), 'sb_turn_times')
+        return dict(zip(('ms_expand', 'ms_survive', 'ms_mt', 'ms_emit', 'ms_select', 'ms_gather', 'ms_total'),
+                        (float(x) for x in out)))
 
     def num_turns(self) -> int:
         n = C.c_int32()

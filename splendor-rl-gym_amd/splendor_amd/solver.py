@@ -152,7 +152,7 @@ class State:
     # ------------------------------------------------------------ solve (src/solver.py:390-464)
     def solve(self, goal_pts: int = 15, *, use_heuristic: bool = False, heuristic_name: str = 'simple',
               beam_width: int = 300_000, verbose: bool = True, device: int = 0,
-              sync_random: bool = True) -> list['State']:
+              sync_random: bool = True, gpus: int = 1) -> list['State']:
         """Solve the game using BFS with optional heuristic beam search, on the MI355X engine.
 
         Same signature, output and printing as the reference; ``device`` picks the
@@ -160,6 +160,9 @@ class State:
         (after one ``randint`` per scored state).  A heuristic registered in
         ``HEURISTICS`` by the user runs as Python on the host over the device's
         next_queue (see ``_host_scores``); the built-in ones run on the device.
+        ``gpus > 1`` shards the beam over that many GPUs (devices ``device`` ..
+        ``device + gpus - 1``), one worker process each (``multi.launch``); same
+        output, same path, same ``random`` state afterwards.
         """
         if verbose:
             print('=' * 60)
@@ -182,6 +185,16 @@ class State:
             hid = L.SB_HEUR_HOST
         st = random.getstate()
         lo, hi = self.packed()
+        if gpus > 1:
+            if hid == L.SB_HEUR_HOST:
+                raise ValueError('a user-registered heuristic scores on the host: solve it with gpus=1')
+            from .multi import launch
+            res = launch({'goal': goal_pts, 'use_heuristic': bool(use_heuristic), 'heuristic': hid,
+                          'beam_width': beam_width, 'mt': list(st[1]), 'root': [lo, hi], 'verbose': verbose,
+                          'device': device}, gpus)
+            if use_heuristic and sync_random:
+                random.setstate((st[0], tuple(int(x) for x in res['mt']), st[2]))
+            return [State.from_packed(a, b) for a, b in res['path']]
         eng = BeamEngine(goal_pts=goal_pts, use_heuristic=use_heuristic, heuristic=hid, beam_width=beam_width,
                          mt_state625=st[1], root_lo=lo, root_hi=hi, device=device)
         try:

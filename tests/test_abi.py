@@ -78,3 +78,17 @@ def test_stale_library_is_refused(tmp_path, monkeypatch):
     import pytest
     with pytest.raises(ImportError, match='stale'):
         _lib.check_fresh(L, _lib.LIB_PATH)
+
+
+def test_sharded_slice_capacity_is_checked():
+    """Sharded own-claim tags hold a rank's local parent rank in 26 bits: a beam whose slice
+    per rank exceeds 2^26 is refused at sb_create (and a larger slice at sbd_expand_launch)."""
+    import numpy as np
+    L = _lib.lib()
+    _lib.ensure_tables()
+    h = ctypes.c_void_p()
+    cfg = _lib.SbConfig(goal_pts=15, use_heuristic=1, heuristic=3, device=0, beam_width=(1 << 27) + 2,
+                        world_size=2, rank=0)
+    rc = L.sb_create(ctypes.byref(cfg), np.zeros(625, np.uint32), 0, 0, ctypes.byref(h))
+    assert rc == _lib.SB_ERR_CAPACITY
+    assert b'2^26' in L.sb_last_error()

@@ -100,3 +100,34 @@ def test_cli_verbose_output_matches_reference(case):
     assert out.returncode == 0, out.stderr
     exp = [ln for ln in g['stdout'].splitlines() if ln not in _BUYS_MESSAGES]
     assert out.stdout.splitlines() == exp
+
+
+def test_gpus_flag():
+    a = build_parser().parse_args(['15', '-u', '--gpus', '4'])
+    assert a.gpus == 4 and build_parser().parse_args(['15']).gpus == 1
+    for bad in (['15', '--gpus', '0'], ['15', '--realistic', '--gpus', '2']):
+        out = subprocess.run([sys.executable, SCRIPT, *bad], capture_output=True, text=True, timeout=120)
+        assert out.returncode == 2 and '--gpus' in out.stderr
+
+
+def test_multi_gpu_launcher_dry_run():
+    """State.solve(gpus=N) / --gpus N start N worker processes with torch.distributed.run (never touching
+    the GPU in the caller); the plumbing on CPU: the workers join one gloo world, rank 0 reports back."""
+    from splendor_amd.multi import launch
+    assert launch({'dry_run': True}, 2) == {'dry_run': True, 'world': 2}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('argv', [['8', '-u', '-H', 'efficiency', '-w', '20000', '--seed', '0'],
+                                  ['10', '-u', '-H', 'balanced', '-w', '3000', '--seed', '0']])
+def test_cli_gpus_2_matches_one_gpu(argv):
+    """`--gpus 2` (2 ranks on one GPU, gloo transport) prints exactly what the single-GPU run prints:
+    banner, every turn= / max_pts= line, the solution."""
+    env = dict(os.environ, SB_DIST_BACKEND='gloo')
+    one = subprocess.run([sys.executable, SCRIPT, *argv], capture_output=True, text=True, timeout=300, env=env)
+    two = subprocess.run([sys.executable, SCRIPT, *argv, '--gpus', '2'], capture_output=True, text=True, timeout=300,
+                         env=env)
+    assert one.returncode == 0, one.stderr[-2000:]
+    assert two.returncode == 0, two.stderr[-2000:]
+    assert '\nSolution:\n' in one.stdout and 'max_pts=' in one.stdout
+    assert two.stdout == one.stdout

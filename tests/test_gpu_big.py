@@ -5,6 +5,9 @@ the pinned C oracle (oracle/make_big_golden.py; the Python reference cannot run 
   * the sharded protocol at W=4M: world 1 (flags bit 1) on C3 (balanced), and world 2 on one GPU (gloo
     transport, HIP per-rank primitives) on C5's heuristic (efficiency) — every turn's beam digest over the
     rank slices in rank order, turn sizes, path and final MT state
+  * C5 itself (goal 15, efficiency, W=32M): the single-GPU engine (queues of >= 2^24 parents: 8-byte
+    descriptors; the visited set rebuilt past 2^32 slots) and the sharded protocol at world 8 on one GPU
+    (4M states per rank, gloo transport, HIP primitives: 8-way owner partition, 8-source claim segments)
 """
 import json
 import os
@@ -17,7 +20,7 @@ import pytest
 import torch.multiprocessing as mp
 
 import oracle_c
-from conftest import golden
+from conftest import golden, golden_exists
 
 pytestmark = pytest.mark.gpu
 
@@ -56,6 +59,15 @@ def _free_port():
     return p
 
 
+def _digest_turn(outdir, t, world):
+    """sha256 digest of turn t's beam over the rank slices in rank order; the slices' files are removed."""
+    fs = [os.path.join(outdir, f'keys_t{t}_r{r}.npy') for r in range(world)]
+    key = np.concatenate([np.load(f) for f in fs])
+    for f in fs:
+        os.remove(f)
+    return oracle_c.beam_digest(key), len(key)
+
+
 def _worker(rank, world, port, cfg, outdir):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -71,7 +83,7 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=True,
                    heuristic=HEURISTIC_IDS[cfg['heuristic']], beam_width=cfg['width'],
-                   mt_state625=random.getstate()[1])
+                   mt_state625=random.getstate()[1], visited_log2=cfg.get('visited_log2', 0))
     solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=True, beam_width=cfg['width'])
     trace = []
     while True:
@@ -80,7 +92,13 @@ def _worker(rank, world, port, cfg, outdir):
         if st['done']:
             break
         np.save(os.path.join(outdir, f'keys_t{len(trace)}_r{rank}.npy'), b.turn_keys(len(trace)))
-    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist()}
+        if cfg.get('digest_inline'):   # wide beams: rank 0 digests each turn as it completes
+            dist.barrier()
+            if rank == 0:
+                st['digest'], st['beam'] = _digest_turn(outdir, len(trace), world)
+            dist.barrier()
+    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist(),
+           'visited_capacity': list(b.visited_capacity())}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     b.close()
@@ -106,3 +124,65 @@ def test_sharded_w4m_oracle_golden(world, name):
     path = [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in res[0]['path']]
     assert path == [p[5] for p in g['path']]
     assert all(oracle_c.mt_fingerprint(r['mt']) == g['final_mt'] for r in res)
+
+
+C5 = 'oracle_g15_efficiency_w32000000_s0.json'
+
+
+@pytest.mark.skipif(not golden_exists(C5), reason='C5 golden not generated')
+def test_c5_w32m_single_gpu_oracle_golden():
+    """C5's width on one MI355X: queues of 32M parents (>= 2^24: the top-k hands the gather 8-byte
+    descriptors, sb_engine.hip desc_payload_ok) and a visited set started at 2^31 slots that must be
+    rebuilt past 2^32 (k_rehash) on the way to about 2G keys."""
+    from splendor_amd import _lib as L
+    from splendor_amd.engine import HEURISTIC_IDS, BeamEngine
+    g = golden(C5)
+    random.seed(g['seed'])
+    eng = BeamEngine(goal_pts=g['goal'], use_heuristic=True, heuristic=HEURISTIC_IDS[g['heuristic']],
+                     beam_width=g['beam_width'], mt_state625=random.getstate()[1], visited_log2=31)
+    t = 0
+    while True:
+        s = eng.step()
+        if s['done']:
+            break
+        t += 1
+        exp = g['turns'][t - 1]
+        assert (s['n_parents'], s['n_raw'], s['n_unique'], s['n_kept']) == \
+            (exp['n_parents'], exp['n_raw'], exp['n_unique'], exp['n_kept']), t
+        _, _, _, key = eng.read_turn(t)
+        assert oracle_c.beam_digest(key) == exp['digest'], f'turn {t}'
+        del key
+    assert t == len(g['turns'])
+    from splendor_amd.codec import decode, state_key, to_signed
+    assert [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in eng.path()] == \
+        [p[5] for p in g['path']]
+    assert oracle_c.mt_fingerprint(eng.mt_state()) == g['final_mt']
+    cap, rebuilds = L.visited_capacity(eng._h)
+    assert eng.visited_size() == g['visited']
+    assert cap > (1 << 32) and rebuilds >= 2, (cap, rebuilds)
+    eng.close()
+
+
+@pytest.mark.skipif(not golden_exists(C5), reason='C5 golden not generated')
+def test_c5_sharded_world8_oracle_golden():
+    """C5 as the 8-GPU job runs it, 8 ranks on one GPU (gloo transport, HIP per-rank primitives, 4M
+    states per rank): every turn's digest over the rank slices, sizes, path, final MT state on every
+    rank; each rank's owner shard starts at 2^28 slots and is rebuilt on the way."""
+    g = golden(C5)
+    world = 8
+    cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
+           'visited_log2': 28, 'digest_inline': True}
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
+        res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
+    turns = [t for t in res[0]['trace'] if not t['done']]
+    assert len(turns) == len(g['turns'])
+    for t, exp in enumerate(g['turns'], 1):
+        a = turns[t - 1]
+        assert (a['n_raw'], a['n_unique'], a['n_kept']) == (exp['n_raw'], exp['n_unique'], exp['n_kept']), t
+        assert (a['digest'], a['beam']) == (exp['digest'], exp['n_kept']), f'turn {t}'
+    from splendor_amd.codec import decode, state_key, to_signed
+    path = [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in res[0]['path']]
+    assert path == [p[5] for p in g['path']]
+    assert all(oracle_c.mt_fingerprint(r['mt']) == g['final_mt'] for r in res)
+    assert all(r['visited_capacity'][1] >= 1 for r in res)

@@ -101,3 +101,45 @@ def test_custom_heuristic_ignored_without_use_heuristic():
         assert path[-1].pts >= 2
     finally:
         S.HEURISTICS.pop('boom')
+
+
+def test_host_scored_topk_arbitrary_keys():
+    """sb_prune's top-k on keys of no particular distribution: mixed signs, a 1e-10 tie-break
+    jitter (thousands of distinct keys inside one 40-bit prefix run), exact ties and -0.0 == 0.0.  The
+    host-scored path sorts on the full key, so the order is the stable sorted(..., reverse=True)."""
+    rng = np.random.default_rng(5)
+    n = 300_000
+    base = rng.choice(np.array([-3.0, -1.0, 0.0, 2.5, 1e6]), n)
+    jit = np.where(rng.random(n) < 0.5, rng.random(n) * 1e-10, 0.0)
+    s = base + jit
+    s[rng.random(n) < 0.01] = -0.0
+    for keep in (n, 4096, 77_777):
+        out = np.zeros(min(n, keep), np.uint32)
+        L.check(L.lib().sb_debug_topk_scores(0, np.ascontiguousarray(s), n, keep, out), 'sb_debug_topk_scores')
+        exp = sorted(range(n), key=s.__getitem__, reverse=True)[:keep]
+        assert out.tolist() == exp, keep
+
+
+def _jitter(state):
+    return state.pts * 2.0 - sum(state.gems) * 0.5 + (random.random() - 0.5) * 1e-9
+
+
+def test_host_heuristic_jitter_solve_vs_pyref():
+    """A user heuristic with a tiny random tie-break (near-equal, mixed-sign scores) through State.solve,
+    against the pure-Python restatement of the reference loop running the same callable."""
+    import pyref
+    S.HEURISTICS['jitter'] = _jitter
+    try:
+        random.seed(3)
+        path = S.State.newgame().solve(goal_pts=8, use_heuristic=True, heuristic_name='jitter', beam_width=3000,
+                                       verbose=False)
+        after = random.getstate()
+        random.seed(3)
+        ps = pyref.PySolve(8, use_heuristic=True, heuristic_name='simple', beam_width=3000, rng=random.Random(0))
+        ps.heur = lambda st, _rng: _jitter(st)
+        while not ps.step()['done']:
+            pass
+        assert [p.hash for p in path] == [s.key for s in ps.path()]
+        assert random.getstate() == after
+    finally:
+        S.HEURISTICS.pop('jitter')
