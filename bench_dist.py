@@ -42,7 +42,7 @@ def main(args):
     json_fd = os.dup(1)
     os.dup2(2, 1)
     from bench import GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, probe_window, step_bytes, timed_steps
-    from splendor_amd.dist import Comm, DistSolve, HipBackend
+    from splendor_amd.dist import Comm, DistSolve, HipBackend, SerializedBackend
     from splendor_amd.engine import HEURISTIC_IDS
     if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
         os.environ.update(RANK='0', LOCAL_RANK='0', WORLD_SIZE='1', MASTER_ADDR='127.0.0.1',
@@ -57,15 +57,20 @@ def main(args):
     if world != args.gpus and not (args.gpus == 1 and os.environ.get('SB_FORCE_DIST') == '1'):
         raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
     W = args.width * world
+    serial = dist.new_group(backend='gloo') if os.environ.get('SB_DIST_SERIALIZE') == '1' and world > 1 else None
 
     def make():
         random.seed(args.seed)
         b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=GOAL, use_heuristic=True,
-                       heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1])
+                       heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1],
+                       visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')))
+        if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend)
+            b = SerializedBackend(b, serial)
         return DistSolve(b, Comm(b.device), goal_pts=GOAL, use_heuristic=True, beam_width=W)
 
     def close(s):
         s.b.close()
+        torch.cuda.synchronize()
 
     def sync_all(_s):
         torch.cuda.synchronize()

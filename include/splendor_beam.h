@@ -60,7 +60,8 @@ typedef struct {
     int32_t flags;             /* bit 0: collect per-kernel timings; bit 1: sharded (sbd_*) mode even at world_size 1;
                                   bit 2 (test): generic first select pass instead of the one folded into the
                                   emission; bit 3 (test): folded pass with its window forced off the keys
-                                  (exercises its fallback) */
+                                  (exercises its fallback); bit 4 (test): grow the visited set at 25% projected
+                                  load instead of 60% (exercises rebuilds of large tables) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Per-rank device time of the sharded step, by protocol phase, from profiles/collect_r3_sharded.sh traces.
+
+Each rank's kernel trace (rocprofv3 --kernel-trace, one process per rank, SB_DIST_SERIALIZE=1 so every
+kernel ran alone on the device) is cut into steps at its k_expand<true> launches (a step's expansion is
+launched at the end of the previous step; the timed window is the last --steps of them).  Kernels are
+assigned to phases by name, k_part_* by position (before the apply: the owner partition of the records;
+after: the rebalance of the kept records).  Prints a table (ms per step, mean over the timed steps and
+ranks, and the slowest rank) and writes it as JSON with --out.
+"""
+import argparse
+import csv
+import json
+import os
+import re
+from collections import defaultdict
+
+PHASES = [
+    ('expand', r'^k_expand<true>|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
+    ('owner partition', r'^k_part_|^k_chunk_counts'),
+    ('owner claims', r'^k_own_'),
+    ('answer bits', r'^k_(un)?pack_bits'),
+    ('apply', r'^k_apply_w|^k_count_masks|^k_counts_i64|^k_total_i64'),
+    ('noise (side stream)', r'^k_mt_'),
+    ('emit', r'^k_emit_w'),
+    ('joint select', r'^k_ds_|^k_tk_'),
+    ('rebalance partition', r'^k_dest|^k_part_'),
+    ('receive sort + gather', r'^k_recv_|^k_iota|^k_os_|^k_fx_|^k_copy_idx'),
+]
+
+
+def short(name):
+    m = re.match(r'(?:void )?(?:sb::)?([A-Za-z_0-9]+(?:<[^>]*>)?)', name)
+    return m.group(1) if m else name[:40]
+
+
+def load(path):
+    rows = []
+    for r in csv.DictReader(open(path)):
+        rows.append((short(r['Kernel_Name']), int(r['Start_Timestamp']), int(r['End_Timestamp'])))
+    rows.sort(key=lambda x: x[1])
+    return rows
+
+
+def find_trace(d):
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith('kernel_trace.csv'):
+                return os.path.join(root, f)
+    raise FileNotFoundError(d)
+
+
+def rank_table(rows, steps):
+    ex = [i for i, r in enumerate(rows) if r[0] == 'k_expand<true>']
+    if len(ex) < steps:
+        raise RuntimeError(f'only {len(ex)} expansions in the trace')
+    starts = ex[-steps:] + [len(rows)]
+    per = defaultdict(float)
+    unknown = defaultdict(float)
+    spans = []
+    for s in range(steps):
+        seg = rows[starts[s]:starts[s + 1]]
+        applied = False
+        for name, t0, t1 in seg:
+            dt = (t1 - t0) / 1e6
+            if name.startswith('k_apply_w'):
+                applied = True
+            ph = None
+            for p, rx in PHASES:
+                if re.search(rx, name):
+                    if p == 'owner partition' and applied:
+                        continue
+                    if p == 'rebalance partition' and not applied:
+                        continue
+                    ph = p
+                    break
+            if ph is None:
+                unknown[name] += dt
+            else:
+                per[ph] += dt
+        spans.append((seg[-1][2] - seg[0][1]) / 1e6)
+    out = {p: per[p] / steps for p, _ in PHASES}
+    out['other'] = sum(unknown.values()) / steps
+    out['device total (engine stream)'] = sum(v for k, v in out.items() if not k.startswith('noise'))
+    return out, {k: v / steps for k, v in unknown.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('dir')
+    ap.add_argument('--world', type=int, required=True)
+    ap.add_argument('--steps', type=int, default=6)
+    ap.add_argument('--out')
+    a = ap.parse_args()
+    ranks = []
+    unk = {}
+    for r in range(a.world):
+        t, u = rank_table(load(find_trace(os.path.join(a.dir, f'r{r}'))), a.steps)
+        ranks.append(t)
+        for k, v in u.items():
+            unk[k] = max(unk.get(k, 0.0), v)
+    keys = list(ranks[0].keys())
+    mean = {k: sum(t[k] for t in ranks) / len(ranks) for k in keys}
+    worst = {k: max(t[k] for t in ranks) for k in keys}
+    print(f'{"phase":34s} {"mean ms":>9s} {"max ms":>9s}')
+    for k in keys:
+        print(f'{k:34s} {mean[k]:9.3f} {worst[k]:9.3f}')
+    if unk:
+        print('unclassified:', {k: round(v, 3) for k, v in unk.items()})
+    if a.out:
+        with open(a.out, 'w') as f:
+            json.dump({'world': a.world, 'steps': a.steps, 'mean_ms': mean, 'max_ms': worst, 'per_rank_ms': ranks,
+                       'unclassified_ms': unk}, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()

@@ -842,7 +842,8 @@ constexpr size_t GROW_RESERVE = (size_t)4 << 30;
 static void grow_table(Engine& E, Entry*& tab, uint64_t& mask, double projected) {
     const uint64_t cap = mask + 1;
     uint64_t ncap = cap;
-    while (projected > GROW_LOAD * (double)ncap && ncap < (1ull << 36)) ncap <<= 1;
+    const double grow_load = (E.cfg.flags & 16) ? 0.25 : GROW_LOAD;   // flags bit 4 (test): eager growth
+    while (projected > grow_load * (double)ncap && ncap < (1ull << 36)) ncap <<= 1;
     if (ncap == cap) return;
     size_t freeb = 0, totalb = 0;
     SB_HIP(hipMemGetInfo(&freeb, &totalb));

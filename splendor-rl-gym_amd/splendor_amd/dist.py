@@ -529,6 +529,33 @@ class DistSolve:
         return out[::-1]
 
 
+class SerializedBackend:
+    """Profiling aid (bench_dist.py with SB_DIST_SERIALIZE=1): several ranks sharing one GPU run their
+    backend calls one rank at a time, each call synchronised before the next rank's, so a kernel trace
+    shows every rank's kernels alone on the device — the device time one rank's own GPU would spend.
+    Results are unchanged (the same calls in the same order per rank)."""
+
+    def __init__(self, backend, group=None):
+        self._b = backend
+        self._g = group if group is not None else dist.new_group(backend='gloo')
+        self._rank, self._world = dist.get_rank(), dist.get_world_size()
+
+    def __getattr__(self, name):
+        attr = getattr(self._b, name)
+        if not callable(attr):
+            return attr
+
+        def call(*a, **k):
+            out = None
+            for r in range(self._world):
+                if r == self._rank:
+                    out = attr(*a, **k)
+                    torch.cuda.synchronize()
+                dist.barrier(group=self._g)
+            return out
+        return call
+
+
 class HipBackend:
     """Per-rank primitives on the MI355X engine (libsplendor_beam.so, sbd_* entry points).
 

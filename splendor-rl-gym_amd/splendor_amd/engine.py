@@ -19,10 +19,10 @@ class BeamEngine:
                  mt_state625, root_lo: int = 0, root_hi: int = 0, device: int = 0, visited_log2: int = 0,
                  timing: bool = False, test_flags: int = 0):
         L.ensure_tables()
-        # test_flags: sb_config.flags bits 2-3 (include/splendor_beam.h), alternative select paths for tests
+        # test_flags: sb_config.flags bits 2-4 (include/splendor_beam.h): alternative select paths, eager growth
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=(1 if timing else 0) | (int(test_flags) & 12), world_size=1, rank=0)
+                         flags=(1 if timing else 0) | (int(test_flags) & 28), world_size=1, rank=0)
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
         if st.shape != (625,):
             raise ValueError('mt_state625 must be random.getstate()[1] (625 words)')

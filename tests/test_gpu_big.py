@@ -132,14 +132,15 @@ C5 = 'oracle_g15_efficiency_w32000000_s0.json'
 @pytest.mark.skipif(not golden_exists(C5), reason='C5 golden not generated')
 def test_c5_w32m_single_gpu_oracle_golden():
     """C5's width on one MI355X: queues of 32M parents (>= 2^24: the top-k hands the gather 8-byte
-    descriptors, sb_engine.hip desc_payload_ok) and a visited set started at 2^31 slots that must be
-    rebuilt past 2^32 (k_rehash) on the way to about 2G keys."""
+    descriptors, sb_engine.hip desc_payload_ok) and a visited set started at 2^31 slots that is rebuilt
+    (k_rehash) to 2^32 and then past it on the way to about 1.5G keys (flags bit 4: growth at 25%
+    projected load, so a 2^32-slot table is itself rebuilt, 64-bit slot indices throughout)."""
     from splendor_amd import _lib as L
     from splendor_amd.engine import HEURISTIC_IDS, BeamEngine
     g = golden(C5)
     random.seed(g['seed'])
     eng = BeamEngine(goal_pts=g['goal'], use_heuristic=True, heuristic=HEURISTIC_IDS[g['heuristic']],
-                     beam_width=g['beam_width'], mt_state625=random.getstate()[1], visited_log2=31)
+                     beam_width=g['beam_width'], mt_state625=random.getstate()[1], visited_log2=31, test_flags=16)
     t = 0
     while True:
         s = eng.step()
