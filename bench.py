@@ -171,7 +171,9 @@ class Window:
         for t in range(self.first):   # setup: turns 0 .. first-1
             if self.look and t == self.first - 1:   # the first window turn's expansion is timed with it
                 self.look(self.eng, False)
+            t0 = time.perf_counter()
             r = self._step(self.eng)
+            _progress(f'setup turn {t}', t0)
             assert not r['done'], 'setup reached the goal'
         if self.look:
             self.look(self.eng, True)
@@ -190,13 +192,23 @@ class Window:
             self.eng = None
 
 
+PROGRESS = os.environ.get('SB_BENCH_PROGRESS') == '1'   # a line per step on stderr (long profiled runs)
+
+
+def _progress(what, t0):
+    if PROGRESS:
+        print(f'[bench] {what} {time.perf_counter() - t0:.3f} s', file=sys.stderr, flush=True)
+
+
 def probe_window(make, step, close, width):
     """Run one seeded solve to its goal: (first saturated turn, window length, turns, moves).  The window
     is the steps whose queue is full and has no goal state (every later step of the solve ends it)."""
     eng = make()
     turn, first, last = 0, None, None
     while True:
+        t0 = time.perf_counter()
         r = step(eng)
+        _progress(f'probe turn {turn}', t0)
         if r['done']:
             break
         if r['n_parents'] >= width and first is None:
@@ -210,7 +222,7 @@ def probe_window(make, step, close, width):
     return first, last - first + 1, turn
 
 
-def timed_steps(win, steps, warmup, sync_all, on_segment=None, sync_engine=None, engine_end=False):
+def timed_steps(win, steps, warmup, sync_all, on_segment=None, sync_engine=None, engine_end=False, on_start=None):
     """Warmup on an engine of its own, then exactly `steps` timed window steps on fresh engines, segment by
     segment (a segment ends where an engine's window ends).  Each segment starts with every stream idle
     and ends with every stream synced (the noise generated inside it for later turns is charged to it);
@@ -227,6 +239,8 @@ def timed_steps(win, steps, warmup, sync_all, on_segment=None, sync_engine=None,
         n = min(steps - len(per), win.left)
         turn0 = win.first + win.length - win.left
         sync_all(win.eng)
+        if on_start:
+            on_start()
         t0 = time.perf_counter()
         seg = []
         for i in range(n):
@@ -246,6 +260,7 @@ def timed_steps(win, steps, warmup, sync_all, on_segment=None, sync_engine=None,
             win.look(win.eng, True)
         if on_segment:
             on_segment(win.eng, turn0, seg)
+        _progress(f'timed segment of {n} steps', t0)
         if os.environ.get('SB_BENCH_SEGDBG'):
             ev = sum(p.get('ms_total', 0.0) for p in seg)
             print(f'segment turns {turn0}..{turn0 + n - 1}: wall {dt * 1e3:.3f} ms (engine stream {t_eng * 1e3:.3f}), '

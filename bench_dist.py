@@ -42,7 +42,7 @@ def main(args):
     json_fd = os.dup(1)
     os.dup2(2, 1)
     from bench import GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, probe_window, step_bytes, timed_steps
-    from splendor_amd.dist import Comm, DistSolve, HipBackend, SerializedBackend
+    from splendor_amd.dist import Comm, DistSolve, HipBackend, SerializedBackend, TimedProxy
     from splendor_amd.engine import HEURISTIC_IDS
     if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
         os.environ.update(RANK='0', LOCAL_RANK='0', WORLD_SIZE='1', MASTER_ADDR='127.0.0.1',
@@ -58,15 +58,20 @@ def main(args):
         raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
     W = args.width * world
     serial = dist.new_group(backend='gloo') if os.environ.get('SB_DIST_SERIALIZE') == '1' and world > 1 else None
+    hostprof = {} if os.environ.get('SB_DIST_HOSTPROF') == '1' else None
 
     def make():
         random.seed(args.seed)
         b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=GOAL, use_heuristic=True,
                        heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1],
-                       visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')))
+                       visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')),
+                       extra_flags=int(os.environ.get('SB_DIST_FLAGS', '0')))   # 32: several ranks on one GPU
         if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend)
             b = SerializedBackend(b, serial)
-        return DistSolve(b, Comm(b.device), goal_pts=GOAL, use_heuristic=True, beam_width=W)
+        comm = Comm(b.device)
+        if hostprof is not None:   # host time inside each backend / collective call (SB_DIST_HOSTPROF=1)
+            b, comm = TimedProxy(b, hostprof), TimedProxy(comm, hostprof)
+        return DistSolve(b, comm, goal_pts=GOAL, use_heuristic=True, beam_width=W)
 
     def close(s):
         s.b.close()
@@ -83,7 +88,14 @@ def main(args):
         torch.cuda.current_stream().synchronize()
 
     per, el, el_eng, segs = timed_steps(win, args.steps, args.warmup, sync_all, sync_engine=sync_engine,
-                                        engine_end=args.engine_stream_end)
+                                        engine_end=args.engine_stream_end,
+                                        on_start=hostprof.clear if hostprof is not None else None)
+    if hostprof is not None and rank == 0:   # the last timed segment's calls (cleared at each segment start)
+        tot = sum(v[1] for v in hostprof.values())
+        print(f'hostprof: last segment ({segs[-1]} steps; all segments {el * 1e3:.3f} ms wall over {len(per)} steps); '
+              f'inside calls {tot * 1e3:.3f} ms', file=sys.stderr)
+        for k, (c, t) in sorted(hostprof.items(), key=lambda kv: -kv[1][1]):
+            print(f'hostprof {k:24s} calls {c:6d} ms {t * 1e3:9.3f}', file=sys.stderr)
     win.close()
     comm = Comm(torch.device('cuda', dev))
     el_max = float(comm.allreduce(np.array([int(el * 1e9)]), dist.ReduceOp.MAX)[0]) / 1e9

@@ -61,7 +61,9 @@ typedef struct {
                                   bit 2 (test): generic first select pass instead of the one folded into the
                                   emission; bit 3 (test): folded pass with its window forced off the keys
                                   (exercises its fallback); bit 4 (test): grow the visited set at 25% projected
-                                  load instead of 60% (exercises rebuilds of large tables) */
+                                  load instead of 60% (exercises rebuilds of large tables); bit 5: sharded record
+                                  buffers for 48 raw children per parent instead of the worst case (several
+                                  ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;

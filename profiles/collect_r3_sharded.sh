@@ -14,7 +14,7 @@ PORT=$((20000 + RANDOM % 20000))
 pids=()
 for r in $(seq 0 $((N - 1))); do
     RANK=$r LOCAL_RANK=$r WORLD_SIZE=$N LOCAL_WORLD_SIZE=$N MASTER_ADDR=127.0.0.1 MASTER_PORT=$PORT \
-    SB_DIST_BACKEND=gloo SB_DIST_SERIALIZE=1 SB_VISITED_LOG2=$VL SB_DIST_PHASES=1 \
+    SB_DIST_BACKEND=gloo SB_DIST_SERIALIZE=1 SB_VISITED_LOG2=$VL SB_BENCH_PROGRESS=1 SB_DIST_FLAGS=32 \
     timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d "$OUT/r$r" -o run -- \
         python3 bench.py --gpus "$N" --no-cpu-baseline --steps 6 --warmup 0 > "$OUT/bench_r$r.json" 2> "$OUT/r$r.err" &
     pids+=($!)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 3: C5 world-8 parity (8 ranks on one GPU, compact record buffers), host-time profile of the
+# sharded step at world 1, then serialised per-rank traces at world 2 and 8
+O=${1:-gpurun_out/r3d}; mkdir -p $O/w1
+timeout -k 10 1000 python3 -u -m pytest tests/test_gpu_big.py -k c5_sharded -x -v -s --timeout 900 --timeout-method thread > $O/tests_c5w8.log 2>&1
+rc=$?
+tail -3 $O/tests_c5w8.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+SB_FORCE_DIST=1 SB_DIST_HOSTPROF=1 timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --steps 12 --warmup 2 > $O/w1/bench_hostprof.json 2> $O/w1/hostprof.txt || exit $?
+grep hostprof $O/w1/hostprof.txt
+bash profiles/collect_r3_sharded.sh $O/w2 2 30 || exit $?
+python3 profiles/sharded_table.py $O/w2 --world 2 --steps 6 --out $O/w2_table.json
+bash profiles/collect_r3_sharded.sh $O/w8 8 29 || exit $?
+python3 profiles/sharded_table.py $O/w8 --world 8 --steps 6 --out $O/w8_table.json

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err,
                                                   uint32_t* __restrict__ work, uint32_t me, uint32_t world,
                                                   const uint32_t* __restrict__ roff, uint64_t* __restrict__ rkey,
-                                                  uint8_t* __restrict__ rdig) {
+                                                  uint8_t* __restrict__ rdig, uint64_t rcap) {
     __shared__ XpShared S;
     load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -495,6 +495,10 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                     const uint32_t ord = (uint32_t)((w0 > 0 ? __popcll(ms[0]) : 0) + (w0 > 1 ? __popcll(ms[1]) : 0) +
                                                     __popcll(ms[w0] & below));
                     const uint32_t ri = S.proff[s] + ord;
+                    if (ri >= rcap) {   // compact record buffers (flags bit 5) overflowed: sbd_expand_counts fails
+                        atomicOr(err, 64u);
+                        continue;
+                    }
                     const uint32_t ow = owner_of(key[u], world);
                     rdig[ri] = ow == me ? (uint8_t)0xFF : (uint8_t)ow;
                     if (ow != me) {
@@ -822,6 +826,7 @@ struct Engine {
     int n_grow = 0;
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
     bool records = true;                  // sharded: this turn made records for other owners (world > 1)
+    int64_t rec_per_parent = MAX_CHILDREN;   // sharded record slots per parent (flags bit 5: 48, overflow checked)
     bool apply_pending = false;           // sharded: sbd_apply done, sbd_apply_finish not yet
     bool expand_pending = false;          // sharded: sbd_expand_launch done, sbd_expand_counts not yet
     int expand_world = 1;
@@ -879,6 +884,7 @@ static void check_err_word(Engine& E) {
     if (e & 8u) throw HipError{hipErrorLaunchFailure, "sharded answers do not match the parents' move counts"};
     if (e & 16u) throw HipError{hipErrorInvalidValue, "heuristic returned NaN: no stable sort order exists"};
     if (e & 32u) throw HipError{hipErrorLaunchFailure, "top-k sort fix-up: more distinct keys in one prefix run than it holds"};
+    if (e & 64u) throw HipError{hipErrorOutOfMemory, "sharded records exceed the compact record buffers (flags bit 5)"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -902,9 +908,9 @@ static void preallocate_dist(Engine& E) {
     E.cand.ensure(wl * 3);
     E.lost.ensure(wl * 3);
     if (E.cfg.world_size > 1) {   // record buffers for the worst case: sbd_expand_launch needs no host count
-        E.cand_key.ensure(wl * MAX_CHILDREN);
-        E.cand_pos.ensure(wl * MAX_CHILDREN);
-        E.digit.ensure(wl * MAX_CHILDREN);
+        E.cand_key.ensure(wl * E.rec_per_parent);
+        E.cand_pos.ensure(wl * E.rec_per_parent);
+        E.digit.ensure(wl * E.rec_per_parent);
     }
     E.own_lost.ensure(nr / 64 + 1);
     E.nlo.ensure(nu);
@@ -987,7 +993,7 @@ static void launch_front(Engine& E) {
         // walk ran blocks a million ranks apart side by side: more displaced same-turn claims)
         hipLaunchKernelGGL(k_expand<false>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
                            cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1,
-                           E.d_small + 264, 0u, 1u, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint8_t*)nullptr);
+                           E.d_small + 264, 0u, 1u, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint8_t*)nullptr, 0ull);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)
@@ -1341,6 +1347,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
             const int64_t wl = cfg->beam_width / std::max(1, (int)cfg->world_size) + 1;
             E.turn_mem.block_bytes = std::max<size_t>((size_t)256 << 20, (size_t)wl * 4 * 20);
         }
+        if (cfg->flags & 32) E.rec_per_parent = 48;   // compact sharded record buffers (several ranks per GPU)
         E.dev = cfg->device;
         SB_HIP(hipSetDevice(E.dev));
         SB_HIP(hipStreamCreateWithFlags(&E.s, hipStreamNonBlocking));

@@ -556,6 +556,29 @@ class SerializedBackend:
         return call
 
 
+class TimedProxy:
+    """Profiling aid (bench_dist.py with SB_DIST_HOSTPROF=1): host time spent inside each method of the
+    wrapped backend / Comm (calls that wait for the device show their wait here); the step's wall time
+    minus the sum is the Python orchestration between calls."""
+
+    def __init__(self, obj, table):
+        self._o, self._t = obj, table
+
+    def __getattr__(self, name):
+        attr = getattr(self._o, name)
+        if not callable(attr):
+            return attr
+
+        def call(*a, **k):
+            t0 = time.perf_counter()
+            out = attr(*a, **k)
+            e = self._t.setdefault(name, [0, 0.0])
+            e[0] += 1
+            e[1] += time.perf_counter() - t0
+            return out
+        return call
+
+
 class HipBackend:
     """Per-rank primitives on the MI355X engine (libsplendor_beam.so, sbd_* entry points).
 
@@ -566,7 +589,8 @@ class HipBackend:
     """
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
-                 heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0):
+                 heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0,
+                 extra_flags: int = 0):
         import ctypes as C
         from . import _lib as L
         self.C, self.L = C, L
@@ -577,7 +601,7 @@ class HipBackend:
         torch.cuda.set_device(self.device)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2, world_size=int(world), rank=int(rank))
+                         flags=2 | (int(extra_flags) & 48), world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
         L.check(self.lib.sb_create(C.byref(cfg), st, int(root[0]), int(root[1]), C.byref(h)), 'sb_create')

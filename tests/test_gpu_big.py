@@ -83,7 +83,8 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=True,
                    heuristic=HEURISTIC_IDS[cfg['heuristic']], beam_width=cfg['width'],
-                   mt_state625=random.getstate()[1], visited_log2=cfg.get('visited_log2', 0))
+                   mt_state625=random.getstate()[1], visited_log2=cfg.get('visited_log2', 0),
+                   extra_flags=cfg.get('flags', 0))
     solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=True, beam_width=cfg['width'])
     trace = []
     while True:
@@ -96,6 +97,8 @@ def _worker(rank, world, port, cfg, outdir):
             dist.barrier()
             if rank == 0:
                 st['digest'], st['beam'] = _digest_turn(outdir, len(trace), world)
+                print(f'[world {world}] turn {len(trace)}: {st["n_parents"]} parents, digest {st["digest"]}',
+                      flush=True)   # progress (pytest -s) for long runs
             dist.barrier()
     out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist(),
            'visited_capacity': list(b.visited_capacity())}
@@ -168,11 +171,12 @@ def test_c5_w32m_single_gpu_oracle_golden():
 def test_c5_sharded_world8_oracle_golden():
     """C5 as the 8-GPU job runs it, 8 ranks on one GPU (gloo transport, HIP per-rank primitives, 4M
     states per rank): every turn's digest over the rank slices, sizes, path, final MT state on every
-    rank; each rank's owner shard starts at 2^28 slots and is rebuilt on the way."""
+    rank; each rank's owner shard starts at 2^28 slots and is rebuilt on the way; record buffers sized for
+    48 raw children per parent, flags bit 5, since eight ranks share one GPU's HBM)."""
     g = golden(C5)
     world = 8
     cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
-           'visited_log2': 28, 'digest_inline': True}
+           'visited_log2': 28, 'digest_inline': True, 'flags': 32}   # 8 ranks share one GPU's HBM
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
