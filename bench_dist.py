@@ -57,7 +57,7 @@ def main(args):
     if world != args.gpus and not (args.gpus == 1 and os.environ.get('SB_FORCE_DIST') == '1'):
         raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
     W = args.width * world
-    serial = dist.new_group(backend='gloo') if os.environ.get('SB_DIST_SERIALIZE') == '1' and world > 1 else None
+    serial = os.environ.get('SB_DIST_SERIALIZE') == '1' and world > 1
     hostprof = {} if os.environ.get('SB_DIST_HOSTPROF') == '1' else None
 
     def make():
@@ -67,7 +67,7 @@ def main(args):
                        visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')),
                        extra_flags=int(os.environ.get('SB_DIST_FLAGS', '0')))   # 32: several ranks on one GPU
         if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend)
-            b = SerializedBackend(b, serial)
+            b = SerializedBackend(b)
         comm = Comm(b.device)
         if hostprof is not None:   # host time inside each backend / collective call (SB_DIST_HOSTPROF=1)
             b, comm = TimedProxy(b, hostprof), TimedProxy(comm, hostprof)

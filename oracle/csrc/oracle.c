@@ -363,6 +363,7 @@ typedef struct {
     turn_t* turns; int nturns, capturns;
     int spill_fd;    /* >= 0: earlier turns' states live in this (unlinked) file */
     int64_t spill_end;
+    FILE* key_dump;  /* analysis: every turn's next_queue score keys (u64, next_queue order) appended here */
 } oc_handle;
 
 typedef struct {
@@ -402,6 +403,12 @@ int oc_set_lean(oc_handle* h, int log2_slots, const char* dir) {
         h->spill_fd = fd;
     }
     return 0;
+}
+
+/* analysis aid (profiles/analysis/): append each turn's next_queue score keys to `path` */
+int oc_dump_keys(oc_handle* h, const char* path) {
+    h->key_dump = fopen(path, "wb");
+    return h->key_dump ? 0 : -1;
 }
 
 static int spill_turn(oc_handle* h, int t) {
@@ -447,6 +454,7 @@ void oc_destroy(oc_handle* h) {
     if (!h) return;
     for (int t = 0; t < h->nturns; t++) { free(h->turns[t].st); free(h->turns[t].par); }
     if (h->spill_fd >= 0) close(h->spill_fd);
+    if (h->key_dump) fclose(h->key_dump);
     free(h->turns); free(h->visited.slot); free(h);
 }
 
@@ -565,6 +573,11 @@ int oc_step(oc_handle* h, oc_stats* out) {
         for (int64_t i = 0; i < nq; i++) {
             double sc = score_base(nxt[i], h->heuristic, (double)mt_randint100(&h->mt) * 0.01);
             memcpy(&key[i], &sc, 8);   /* scores are > 0: IEEE bits order == numeric order */
+        }
+        if (h->key_dump) {
+            int64_t nn = nq;
+            fwrite(&nn, 8, 1, h->key_dump);
+            fwrite(key, 8, (size_t)nq, h->key_dump);
         }
         int64_t W = nq < h->beam_width ? nq : h->beam_width;
         uint32_t* cand = (uint32_t*)malloc(sizeof(uint32_t) * (W ? W : 1));

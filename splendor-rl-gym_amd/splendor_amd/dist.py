@@ -531,27 +531,32 @@ class DistSolve:
 
 class SerializedBackend:
     """Profiling aid (bench_dist.py with SB_DIST_SERIALIZE=1): several ranks sharing one GPU run their
-    backend calls one rank at a time, each call synchronised before the next rank's, so a kernel trace
-    shows every rank's kernels alone on the device — the device time one rank's own GPU would spend.
-    Results are unchanged (the same calls in the same order per rank)."""
+    backend calls under one inter-process lock (flock on `lock_path`), each call synchronised before the
+    lock is released, so a kernel trace shows every rank's kernels alone on the device — the device time
+    one rank's own GPU would spend.  Ranks may make different calls (e.g. pack_bits only for non-empty
+    segments): the lock needs no matching call counts.  Results are unchanged."""
 
-    def __init__(self, backend, group=None):
+    def __init__(self, backend, lock_path=None):
+        import tempfile
         self._b = backend
-        self._g = group if group is not None else dist.new_group(backend='gloo')
-        self._rank, self._world = dist.get_rank(), dist.get_world_size()
+        path = lock_path or os.path.join(tempfile.gettempdir(),
+                                         f'sb_serial_{os.environ.get("MASTER_PORT", "0")}.lock')
+        self._fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o600)
 
     def __getattr__(self, name):
+        import fcntl
         attr = getattr(self._b, name)
         if not callable(attr):
             return attr
 
         def call(*a, **k):
-            out = None
-            for r in range(self._world):
-                if r == self._rank:
-                    out = attr(*a, **k)
+            fcntl.flock(self._fd, fcntl.LOCK_EX)
+            try:
+                out = attr(*a, **k)
+                if torch.cuda.is_available():
                     torch.cuda.synchronize()
-                dist.barrier(group=self._g)
+            finally:
+                fcntl.flock(self._fd, fcntl.LOCK_UN)
             return out
         return call
 

@@ -46,6 +46,9 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     st = random.getstate()[1]
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
+    if cfg.get('serialize'):   # the profiling wrapper (bench_dist.py SB_DIST_SERIALIZE=1) changes nothing
+        from splendor_amd.dist import SerializedBackend
+        b = SerializedBackend(b)
     solve = DistSolve(b, Comm(torch.device('cpu')), goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                       beam_width=cfg['width'])
     if cfg.get('toggle'):   # bench.py's window edges: the next turn's expansion deferred to the next step
@@ -81,6 +84,8 @@ CASES = [
     (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True}),
     # lookahead off every third step (the expansion launched by the step that needs it)
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True}),
+    # the per-rank profiling wrapper (one rank's backend calls at a time) changes no result
+    (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'serialize': True}),
 ]
 
 
