@@ -827,6 +827,7 @@ struct Engine {
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
     bool records = true;                  // sharded: this turn made records for other owners (world > 1)
     int64_t rec_per_parent = MAX_CHILDREN;   // sharded record slots per parent (flags bit 5: 48, overflow checked)
+    size_t rcap_turn = 0;                 // sharded: record slots of the expansion in flight
     bool apply_pending = false;           // sharded: sbd_apply done, sbd_apply_finish not yet
     bool expand_pending = false;          // sharded: sbd_expand_launch done, sbd_expand_counts not yet
     int expand_world = 1;
