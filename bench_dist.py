@@ -76,6 +76,7 @@ def main(args):
     def close(s):
         s.b.close()
         torch.cuda.synchronize()
+        torch.cuda.empty_cache()   # the exchange buffers of this solve go back to the device
 
     def sync_all(_s):
         torch.cuda.synchronize()
