@@ -194,6 +194,10 @@ int sbd_goal_table(sb_engine* e, uint32_t* first256);
  * chunk_owner_counts[nchunk][world] = records per chunk and owner, *n_raw = successors generated. */
 int sbd_expand_launch(sb_engine* e, int32_t world);
 int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts, int64_t* n_raw);
+/* world 1 (no records, no exchange to size): go on without waiting for the expansion; *n_raw is read by
+ * sbd_raw_total after the caller's next wait on the engine stream (sbd_apply's count). */
+int sbd_expand_defer(sb_engine* e);
+int sbd_raw_total(sb_engine* e, int64_t* n_raw);
 /* the record keys grouped by owner, (parent, ordinal) order inside a group (d_tag unused: tags are
  * implicit in the order) */
 int sbd_pack(sb_engine* e, uint64_t* d_key, uint64_t* d_tag);

@@ -818,6 +818,7 @@ struct Engine {
     int64_t own_n = 0;                    // sharded: records claimed at this owner this turn
     DBuf<uint64_t> dsel, dsel_c;          // joint select: prefixes / histograms, candidate keys
     DBuf<uint32_t> dsel_t;                // joint select: compaction tile offsets
+    DBuf<uint32_t> dsel_ci;               // joint select: candidates' indices (the tie counts per tile)
     int dsel_npos = 1;                    // joint select: positions (histogram rows)
     DBuf<uint64_t> rkey;                  // sharded receive: keys of the received records
     DBuf<uint8_t> digit;
@@ -830,6 +831,7 @@ struct Engine {
     size_t rcap_turn = 0;                 // sharded: record slots of the expansion in flight
     bool apply_pending = false;           // sharded: sbd_apply done, sbd_apply_finish not yet
     bool expand_pending = false;          // sharded: sbd_expand_launch done, sbd_expand_counts not yet
+    bool raw_pending = false;             // sharded world 1: sbd_expand_defer done, sbd_raw_total not yet
     int expand_world = 1;
     uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
     std::vector<int64_t> srcb;            // sharded: first answer index of each source's records this turn
@@ -919,6 +921,7 @@ static void preallocate_dist(Engine& E) {
     E.npar.ensure(nu);
     E.skey.ensure(nu);
     E.dsel_c.ensure(nu);
+    E.dsel_ci.ensure(nu);
     // the joint select's tile counts, tie tiles and destinations grow with the turn's unique children:
     // a mid-step regrowth (hipFree) waits for the device to drain (0.2-0.5 ms each, sbd_sel_compact /
     // sbd_partition); tiles of 4096 keys (sb_dist.inc PT_TILE)
@@ -1628,6 +1631,7 @@ void sb_destroy(sb_engine* h) {
     E.desc.release();
     E.rslot.release();
     E.cand.release();
+    E.lost.release();
     E.surv.release();
     E.cnt.release();
     E.off.release();
@@ -1653,6 +1657,7 @@ void sb_destroy(sb_engine* h) {
     E.dsel.release();
     E.dsel_c.release();
     E.dsel_t.release();
+    E.dsel_ci.release();
     E.rkey.release();
     E.part_hist.release();
     E.digit.release();

@@ -53,7 +53,6 @@ constexpr int64_t TK_WRITE_GRID = SB_TK_WRITE_GRID;           // candidate passe
 #define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
 #endif
 constexpr int OS_PREFIX_BITS = SB_SORT_PREFIX_BITS;
-constexpr int OS_MAX_PASSES = (OS_PREFIX_BITS + 7) / 8;
 
 
 // device state (u64 words)

@@ -365,6 +365,20 @@ class DistSolve:
         if self._front_deferred:
             b.expand_launch(c.world)
             self._front_deferred = False
+        if c.world == 1 and hasattr(b, 'expand_defer'):
+            # one rank: no records, nothing to size, so no wait for the expansion; its raw count comes with
+            # the apply's wait below
+            b.expand_defer()
+            b.owner_begin(0, [0])
+            ret = self._ret0 if getattr(self, '_ret0', None) is not None else b.answer_buffer(0)
+            self._ret0 = ret
+            b.owner_finish(ret)
+            self._mark(st, 'expand')
+            all_n = c.gather_dev(b.apply(ret[:0])).astype(np.int64)
+            st['n_raw'] = b.raw_total()
+            b.apply_finish(int(all_n[0]))
+            self._mark(st, 'dedup_exchange')
+            return self._post_dedup(st, all_n, off)
         cc, n_raw = b.expand_counts(C)                              # (C, world) records per chunk, owner
         M = c.allgather_array(np.concatenate([cc.ravel(), [n_raw]]))
         st['n_raw'] = int(M[:, -1].sum())
@@ -424,6 +438,11 @@ class DistSolve:
         all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
+        return self._post_dedup(st, all_n, off)
+
+    def _post_dedup(self, st, all_n, off):
+        """noise, emission, joint select, rebalance and receive of a step (after the dedup exchange)."""
+        c, b = self.c, self.b
         k_off = int(all_n[:c.rank].sum())
         N = int(all_n.sum())
         st['n_unique'] = N
@@ -455,7 +474,10 @@ class DistSolve:
             dest_dev = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
         rec = b.pack_kept(all_n[c.rank])   # enqueued ahead of the counts' round trip
-        dest_counts, recv = c.alltoall_counts_dev(dest_dev)
+        if c.world == 1:   # every kept record stays: K of them, known here (no round trip)
+            dest_counts = recv = np.array([K], dtype=np.int64)
+        else:
+            dest_counts, recv = c.alltoall_counts_dev(dest_dev)
         self._mark(st, 'pack_kept')
         if c.world > 1:   # records arrive source rank by source rank; this rank's own are copied
             me = c.rank
@@ -626,6 +648,8 @@ class HipBackend:
         lib.sbd_goal_table.argtypes = [vp, vp]
         lib.sbd_expand_launch.argtypes = [vp, i32]
         lib.sbd_expand_counts.argtypes = [vp, i32, vp, p64]
+        lib.sbd_expand_defer.argtypes = [vp]
+        lib.sbd_raw_total.argtypes = [vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
         lib.sbd_owner_begin.argtypes = [vp, i64, i32, vp]
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
@@ -722,6 +746,15 @@ class HipBackend:
                   'sbd_expand_counts')
         self.owner_counts = counts.reshape(nchunk, self.world_x).sum(axis=0)
         return counts.reshape(nchunk, self.world_x), nraw.value
+
+    def expand_defer(self):
+        """World 1: go on without waiting for the expansion (raw_total() after the next wait)."""
+        self._chk(self.lib.sbd_expand_defer(self.h), 'sbd_expand_defer')
+
+    def raw_total(self) -> int:
+        nraw = self.C.c_int64()
+        self._chk(self.lib.sbd_raw_total(self.h, self.C.byref(nraw)), 'sbd_raw_total')
+        return nraw.value
 
     def _empty(self, n, dtype=torch.int64):
         return torch.empty(int(n), dtype=dtype, device=self.device)
