@@ -357,7 +357,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                                                   unsigned long long* __restrict__ nraw_total, uint32_t* __restrict__ err,
                                                   uint32_t* __restrict__ work, uint32_t me, uint32_t world,
                                                   const uint32_t* __restrict__ roff, uint64_t* __restrict__ rkey,
-                                                  uint8_t* __restrict__ rdig, uint64_t rcap) {
+                                                  uint8_t* __restrict__ rdig, uint64_t rcap, uint8_t* __restrict__ rdsc) {
     __shared__ XpShared S;
     load_enum_lds(T, S.card, S.mlo, S.mhi, S.alo, S.ahi, S.pdelta);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
                     rdig[ri] = ow == me ? (uint8_t)0xFF : (uint8_t)ow;
                     if (ow != me) {
                         rkey[ri] = key[u];
+                        rdsc[ri] = (uint8_t)dsc;   // the apply maps this record's answer to its move directly
                         continue;
                     }
                 }
@@ -822,6 +823,7 @@ struct Engine {
     int dsel_npos = 1;                    // joint select: positions (histogram rows)
     DBuf<uint64_t> rkey;                  // sharded receive: keys of the received records
     DBuf<uint8_t> digit;
+    DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
     // visited-set growth (grow_table): largest raw children per parent seen so far, tables rebuilt
     double raw_ratio = 32.0;
     int n_grow = 0;
@@ -914,6 +916,7 @@ static void preallocate_dist(Engine& E) {
         E.cand_key.ensure(wl * E.rec_per_parent);
         E.cand_pos.ensure(wl * E.rec_per_parent);
         E.digit.ensure(wl * E.rec_per_parent);
+        E.rdsc.ensure(wl * E.rec_per_parent);
     }
     E.own_lost.ensure(nr / 64 + 1);
     E.nlo.ensure(nu);
@@ -997,7 +1000,8 @@ static void launch_front(Engine& E) {
         // walk ran blocks a million ranks apart side by side: more displaced same-turn claims)
         hipLaunchKernelGGL(k_expand<false>, dim3(grid_cap(n, XP_PAR, SB_XP_GRID_CAP)), dim3(XP_NT), 0, E.s, E.d_tables,
                            cur.lo, cur.hi, n, E.tab, E.tab_mask, turn_tag, E.cand.p, E.lost.p, E.d_nraw, E.d_small + 1,
-                           E.d_small + 264, 0u, 1u, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint8_t*)nullptr, 0ull);
+                           E.d_small + 264, 0u, 1u, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint8_t*)nullptr, 0ull,
+                           (uint8_t*)nullptr);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0)
@@ -1661,6 +1665,7 @@ void sb_destroy(sb_engine* h) {
     E.rkey.release();
     E.part_hist.release();
     E.digit.release();
+    E.rdsc.release();
     if (E.d_tables) (void)hipFree(E.d_tables);
     if (E.d_small) (void)hipFree(E.d_small);
     if (E.d_nraw) (void)hipFree(E.d_nraw);
