@@ -66,9 +66,10 @@ def main(args):
                        heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1],
                        visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')),
                        extra_flags=int(os.environ.get('SB_DIST_FLAGS', '0')))   # 32: several ranks on one GPU
-        if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend)
-            b = SerializedBackend(b)
         comm = Comm(b.device)
+        if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend),
+            b = SerializedBackend(b)   # gloo's staging copies under the same lock
+            comm.devlock = b.lock
         if hostprof is not None:   # host time inside each backend / collective call (SB_DIST_HOSTPROF=1)
             b, comm = TimedProxy(b, hostprof), TimedProxy(comm, hostprof)
         return DistSolve(b, comm, goal_pts=GOAL, use_heuristic=True, beam_width=W)

@@ -55,15 +55,26 @@ class Comm:
         # host-side metadata (the turn sync: slice sizes + goal tables) goes over a gloo group: it runs
         # while the expansion occupies every CU, which a device collective would have to wait for
         self.meta = dist.new_group(backend='gloo') if self.world > 1 else None
+        self.devlock = None   # profiling (SerializedBackend.lock): gloo's staging copies under the device lock
+
+    def _cp(self, fn):
+        """A device copy of the gloo staging; under the profiling device lock when one is set."""
+        if self.devlock is None:
+            return fn()
+        with self.devlock():
+            out = fn()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            return out
 
     def _to(self, t):
-        return t.cpu() if self.cpu_coll else t
+        return self._cp(lambda: t.cpu()) if self.cpu_coll else t
 
     def _back(self, t):
-        return t.to(self.device) if self.cpu_coll and self.device.type != 'cpu' else t
+        return self._cp(lambda: t.to(self.device)) if self.cpu_coll and self.device.type != 'cpu' else t
 
     def allreduce(self, arr: np.ndarray, op) -> np.ndarray:
-        t = self._to(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device))
+        t = self._to(self._cp(lambda: torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device)))
         dist.all_reduce(t, op=op)
         return t.cpu().numpy()
 
@@ -80,7 +91,7 @@ class Comm:
     def allgather_int(self, v: int) -> np.ndarray:
         if self.world == 1:
             return np.array([int(v)], dtype=np.int64)
-        t = torch.tensor([int(v)], dtype=torch.int64, device=self.device)
+        t = self._cp(lambda: torch.tensor([int(v)], dtype=torch.int64, device=self.device))
         return self._gather_flat(t).cpu().numpy().astype(np.int64)
 
     def gather_dev(self, t: torch.Tensor) -> np.ndarray:
@@ -116,10 +127,10 @@ class Comm:
         after it.  gloo (no list all_to_all) packs the pieces and completes at once."""
         out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=pieces[0].device)
         if self.cpu_coll:
-            send = torch.cat([p.cpu() for p in pieces])
+            send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             r = torch.empty(int(sum(recv_sizes)), dtype=send.dtype)
             dist.all_to_all_single(r, send, [int(x) for x in recv_sizes], [int(p.numel()) for p in pieces])
-            out.copy_(r.to(out.device))
+            self._cp(lambda: out.copy_(r.to(out.device)))
             return out, None
         outs = list(out.split([int(x) for x in recv_sizes]))
         return out, dist.all_to_all(outs, list(pieces), async_op=True)
@@ -127,12 +138,15 @@ class Comm:
     def alltoall_into(self, pieces, outs):
         """all_to_all of pieces[o] (views) to rank o, received straight into the views outs[o]."""
         if self.cpu_coll:
-            send = torch.cat([p.cpu() for p in pieces])
+            send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             rows = [int(o.shape[0]) for o in outs]
             r = torch.empty((sum(rows),) + tuple(outs[0].shape[1:]), dtype=send.dtype)
             dist.all_to_all_single(r, send, rows, [int(p.shape[0]) for p in pieces])
-            for o, x in zip(outs, r.split(rows)):
-                o.copy_(x.to(o.device))
+
+            def back():
+                for o, x in zip(outs, r.split(rows)):
+                    o.copy_(x.to(o.device))
+            self._cp(back)
             return
         dist.all_to_all(list(outs), list(pieces))
 
@@ -146,9 +160,9 @@ class Comm:
         if self.world == 1:
             return
         if self.cpu_coll:
-            x = t.cpu()
+            x = self._cp(lambda: t.cpu())
             dist.all_reduce(x, op=op)
-            t.copy_(x.to(t.device))
+            self._cp(lambda: t.copy_(x.to(t.device)))
         else:
             dist.all_reduce(t, op=op)
 
@@ -163,7 +177,7 @@ class Comm:
             out = [torch.empty_like(t) for _ in range(self.world)]
             dist.all_gather(out, t, group=self.meta)
             return torch.stack(out).numpy()
-        t = torch.from_numpy(a).to(self.device)
+        t = self._cp(lambda: torch.from_numpy(a).to(self.device))
         return self._gather_flat(t).cpu().numpy().reshape(self.world, len(a))
 
     def allgather_tensor(self, t: torch.Tensor) -> torch.Tensor:
@@ -171,7 +185,7 @@ class Comm:
         return self._back(self._gather_flat(t).reshape((self.world,) + tuple(t.shape)))
 
     def broadcast_ints(self, vals, src: int) -> list[int]:
-        t = self._to(torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device))
+        t = self._to(self._cp(lambda: torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)))
         dist.broadcast(t, src)
         return [int(x) for x in t.cpu().tolist()]
 
@@ -565,20 +579,30 @@ class SerializedBackend:
                                          f'sb_serial_{os.environ.get("MASTER_PORT", "0")}.lock')
         self._fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o600)
 
-    def __getattr__(self, name):
+    def lock(self):
+        """The inter-process device lock as a context manager (Comm.devlock: gloo's staging copies)."""
+        import contextlib
         import fcntl
+
+        @contextlib.contextmanager
+        def held():
+            fcntl.flock(self._fd, fcntl.LOCK_EX)
+            try:
+                yield
+            finally:
+                fcntl.flock(self._fd, fcntl.LOCK_UN)
+        return held()
+
+    def __getattr__(self, name):
         attr = getattr(self._b, name)
         if not callable(attr):
             return attr
 
         def call(*a, **k):
-            fcntl.flock(self._fd, fcntl.LOCK_EX)
-            try:
+            with self.lock():
                 out = attr(*a, **k)
                 if torch.cuda.is_available():
                     torch.cuda.synchronize()
-            finally:
-                fcntl.flock(self._fd, fcntl.LOCK_UN)
             return out
         return call
 
