@@ -50,7 +50,10 @@ def main(args):
     backend = os.environ.get('SB_DIST_BACKEND', 'nccl')
     local = int(os.environ.get('LOCAL_RANK', '0'))
     ndev = torch.cuda.device_count()
-    dev = local if backend == 'nccl' else local % max(ndev, 1)
+    # one GPU per rank; gloo (tests) or SB_DIST_SHARE_GPU=1 (probing RCCL on a one-GPU box) wrap ranks onto
+    # the visible GPUs
+    share = backend != 'nccl' or os.environ.get('SB_DIST_SHARE_GPU') == '1'
+    dev = local % max(ndev, 1) if share else local
     torch.cuda.set_device(dev)
     dist.init_process_group(backend, device_id=torch.device('cuda', dev) if backend == 'nccl' else None)
     rank, world = dist.get_rank(), dist.get_world_size()
