@@ -63,7 +63,9 @@ typedef struct {
                                   (exercises its fallback); bit 4 (test): grow the visited set at 25% projected
                                   load instead of 60% (exercises rebuilds of large tables); bit 5: sharded record
                                   buffers for 48 raw children per parent instead of the worst case (several
-                                  ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY) */
+                                  ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY); bit 6: the
+                                  caller expands with sbd_expand_launch_into (no raw-position key buffer is
+                                  preallocated) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -178,6 +180,13 @@ int sb_debug_scores(int32_t device, int32_t heuristic, const uint64_t* lo, const
 int sb_debug_topk(int32_t device, const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx);
 /* sb_prune's host-scored prune alone: f64 scores (any sign or spacing) -> stable descending order. */
 int sb_debug_topk_scores(int32_t device, const double* scores, int64_t n, int64_t keep, uint32_t* out_idx);
+/* Diagnostic (profiles/expand_bench.py): device time (ms, averaged over reps) of the expansion's variants on
+ * a single-GPU engine's current queue whose expansion is not launched yet (sb_set_lookahead(e, 0) before
+ * the last sb_step), each on a copy of the visited set: out_ms[0] k_expand (one GPU), [1] sharded
+ * expansion at world 1, [2] at world 8 (rank 0), [3] world 8 owning no child (every key a record),
+ * [4] owner claims of all of [3]'s records, [5] [3] and [4] side by side on two streams, [6] raw count +
+ * scan, [7] raw children.  The engine cannot step after this call. */
+int sb_debug_expand_bench(sb_engine* e, int32_t reps, float* out_ms);
 
 /* ---- sharded mode (cfg.world_size > 1 or flags bit 1): per-rank step primitives; the exchanges
  * between them are the caller's (splendor_amd/dist.py: torch.distributed / RCCL).  Device pointers
@@ -194,6 +203,14 @@ int sbd_goal_table(sb_engine* e, uint32_t* first256);
  * chunk_owner_counts[nchunk][world] = records per chunk and owner, *n_raw = successors generated. */
 int sbd_expand_launch(sb_engine* e, int32_t world);
 int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts, int64_t* n_raw);
+/* The same expansion for world > 1 as one key pass (successors hashed, own ones claimed, every other one
+ * written as a record straight into its owner's region of d_rec: owner o's records at [o * ocap, o * ocap +
+ * count) in (parent, ordinal) order; no separate partition, sbd_pack is then a no-op).  ocap >= the value
+ * sbd_record_capacity returns for the current slice; d_rec holds world * ocap keys (world * ocap < 2^32).
+ * sbd_expand_counts returns chunk_owner_counts as for sbd_expand_launch (chunk j = the records of parents
+ * [j * n / nchunk, (j + 1) * n / nchunk) in 64-parent units). */
+int sbd_record_capacity(sb_engine* e, int32_t world, int64_t* ocap);
+int sbd_expand_launch_into(sb_engine* e, int32_t world, uint64_t* d_rec, int64_t ocap);
 /* world 1 (no records, no exchange to size): go on without waiting for the expansion; *n_raw is read by
  * sbd_raw_total after the caller's next wait on the engine stream (sbd_apply's count). */
 int sbd_expand_defer(sb_engine* e);

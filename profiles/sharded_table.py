@@ -16,7 +16,7 @@ import re
 from collections import defaultdict
 
 PHASES = [
-    ('expand', r'^k_expand<true>|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
+    ('expand', r'^k_expand<true>|^k_keys_sh|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
     ('owner partition', r'^k_part_|^k_chunk_counts'),
     ('owner claims', r'^k_own_'),
     ('answer bits', r'^k_(un)?pack_bits'),
@@ -50,8 +50,34 @@ def find_trace(d):
     raise FileNotFoundError(d)
 
 
-def rank_table(rows, steps):
-    ex = [i for i, r in enumerate(rows) if r[0] == 'k_expand<true>']
+def overlap_flags(rows, others):
+    """True for each kernel of `rows` that overlaps a kernel of another rank in time (the serialisation lock
+    does not cover everything a process puts on the device), using the merged intervals of `others`."""
+    iv = sorted((a, b) for _, a, b in others)
+    merged = []
+    for a, b in iv:
+        if merged and a <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], b)
+        else:
+            merged.append([a, b])
+    import bisect
+    starts = [m[0] for m in merged]
+    out = []
+    for _, a, b in rows:
+        i = bisect.bisect_right(starts, b) - 1
+        out.append(i >= 0 and merged[i][1] > a)
+    return out
+
+
+def rank_table(rows, steps, ovl=None):
+    """ovl: per-row overlap flags; an overlapped kernel counts at the median of its clean instances."""
+    clean = defaultdict(list)
+    if ovl is not None:
+        for (name, t0, t1), o in zip(rows, ovl):
+            if not o:
+                clean[name].append((t1 - t0) / 1e6)
+    med = {k: sorted(v)[len(v) // 2] for k, v in clean.items()}
+    ex = [i for i, r in enumerate(rows) if r[0] in ('k_expand<true>', 'k_keys_sh')]
     if len(ex) < steps:
         raise RuntimeError(f'only {len(ex)} expansions in the trace')
     starts = ex[-steps:] + [len(rows)]
@@ -60,9 +86,12 @@ def rank_table(rows, steps):
     spans = []
     for s in range(steps):
         seg = rows[starts[s]:starts[s + 1]]
+        segovl = ovl[starts[s]:starts[s + 1]] if ovl is not None else [False] * len(seg)
         applied = False
-        for name, t0, t1 in seg:
+        for (name, t0, t1), o in zip(seg, segovl):
             dt = (t1 - t0) / 1e6
+            if o and name in med:
+                dt = med[name]
             if name.startswith('k_apply_w'):
                 applied = True
             ph = None
@@ -94,8 +123,13 @@ def main():
     a = ap.parse_args()
     ranks = []
     unk = {}
+    allrows = [load(find_trace(os.path.join(a.dir, f'r{r}'))) for r in range(a.world)]
     for r in range(a.world):
-        t, u = rank_table(load(find_trace(os.path.join(a.dir, f'r{r}'))), a.steps)
+        others = [x for q in range(a.world) if q != r for x in allrows[q]]
+        ovl = overlap_flags(allrows[r], others) if a.world > 1 else None
+        if ovl is not None:
+            print(f'rank {r}: {sum(ovl)} of {len(ovl)} kernels overlap another rank\'s (counted at their clean median)')
+        t, u = rank_table(allrows[r], a.steps, ovl)
         ranks.append(t)
         for k, v in u.items():
             unk[k] = max(unk.get(k, 0.0), v)

@@ -838,6 +838,13 @@ struct Engine {
     uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
     std::vector<int64_t> srcb;            // sharded: first answer index of each source's records this turn
     int64_t pending_host = -1;
+    // sharded key pass (sb_keypass.inc, world > 1): the caller's record buffer (world owner regions of ks_ocap
+    // keys), the chunks' look-back words, per-wave scratch, the (chunk, owner) counts + raw total
+    uint64_t* ks_rec = nullptr;
+    uint64_t ks_ocap = 0;
+    bool ks_turn = false;                 // this turn's expansion ran the key pass
+    DBuf<uint64_t> ks_lb, ks_skey;
+    DBuf<uint32_t> ks_sdr, ks_sown, ks_cc;
     double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
 
@@ -913,7 +920,7 @@ static void preallocate_dist(Engine& E) {
     E.cand.ensure(wl * 3);
     E.lost.ensure(wl * 3);
     if (E.cfg.world_size > 1) {   // record buffers for the worst case: sbd_expand_launch needs no host count
-        E.cand_key.ensure(wl * E.rec_per_parent);
+        if (!(E.cfg.flags & 64)) E.cand_key.ensure(wl * E.rec_per_parent);   // bit 6: key pass, caller's regions
         E.cand_pos.ensure(wl * E.rec_per_parent);
         E.digit.ensure(wl * E.rec_per_parent);
         E.rdsc.ensure(wl * E.rec_per_parent);

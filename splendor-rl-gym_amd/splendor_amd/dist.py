@@ -402,7 +402,10 @@ class DistSolve:
         send_key = b.pack()
         self._mark(st, 'pack')
         mine = Mc[me]                                               # my records per chunk, owner
-        ostart = np.concatenate([[0], np.cumsum(mine.sum(axis=0))])  # owner groups in send_key
+        own_sz = mine.sum(axis=0)                                   # my records per owner
+        # owner groups in send_key: contiguous, or the key pass's owner regions (record_starts)
+        rs = b.record_starts() if hasattr(b, 'record_starts') else None
+        ostart = np.concatenate([[0], np.cumsum(own_sz)]) if rs is None else np.asarray(rs, dtype=np.int64)
         ochunk = np.concatenate([np.zeros((1, c.world), np.int64), np.cumsum(mine, axis=0)])
         from_src = Mc[:, :, me]                                     # [source][chunk] records to me
         src_tot = from_src.sum(axis=1)
@@ -431,7 +434,6 @@ class DistSolve:
         b.owner_finish(ret)
         self._mark(st, 'a2a_keys+claim')
         # answers back to the sources, one bit per answer on the wire (8x less than the answer bytes)
-        own_sz = ostart[1:] - ostart[:-1]
         if c.world > 1:
             nb = lambda x: (int(x) + 7) // 8
             sp = np.concatenate([[0], np.cumsum([nb(src_tot[q]) for q in range(c.world)])])
@@ -446,7 +448,7 @@ class DistSolve:
             back = b.answer_buffer(int(ostart[-1]))
             for o in range(c.world):
                 if own_sz[o]:
-                    b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o + 1])])
+                    b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o] + own_sz[o])])
         else:
             back = ret[:0]
         all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
@@ -652,7 +654,8 @@ class HipBackend:
         torch.cuda.set_device(self.device)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 48), world_size=int(world), rank=int(rank))
+                         flags=2 | (int(extra_flags) & 48) | (64 if self.KEYPASS and world > 1 else 0),
+                         world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
         L.check(self.lib.sb_create(C.byref(cfg), st, int(root[0]), int(root[1]), C.byref(h)), 'sb_create')
@@ -672,6 +675,8 @@ class HipBackend:
         lib.sbd_goal_table.argtypes = [vp, vp]
         lib.sbd_expand_launch.argtypes = [vp, i32]
         lib.sbd_expand_counts.argtypes = [vp, i32, vp, p64]
+        lib.sbd_record_capacity.argtypes = [vp, i32, p64]
+        lib.sbd_expand_launch_into.argtypes = [vp, i32, vp, i64]
         lib.sbd_expand_defer.argtypes = [vp]
         lib.sbd_raw_total.argtypes = [vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
@@ -756,10 +761,33 @@ class HipBackend:
         return self.L.visited_capacity(self.h)
 
     # ---------------------------------------------------------------- step primitives
+    KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'   # world > 1: one key pass writing owner regions
+
     def expand_launch(self, world):
-        """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait."""
+        """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait.
+        world > 1: the key pass (sbd_expand_launch_into) writes the records into owner regions of a
+        buffer held here (record_starts()), so pack() has nothing to do."""
         self.world_x = int(world)
+        self.ocap = None
+        if world > 1 and self.KEYPASS:
+            C = self.C
+            oc = C.c_int64()
+            self._chk(self.lib.sbd_record_capacity(self.h, int(world), C.byref(oc)), 'sbd_record_capacity')
+            need = int(world) * oc.value
+            if getattr(self, '_rec', None) is None or self._rec.numel() < need:
+                self._rec = None
+                self._rec = self._empty(need + need // 4)   # slack: regrown rarely
+            self.ocap = oc.value
+            self._chk(self.lib.sbd_expand_launch_into(self.h, int(world), self._rec.data_ptr(), oc.value),
+                      'sbd_expand_launch_into')
+            return
         self._chk(self.lib.sbd_expand_launch(self.h, int(world)), 'sbd_expand_launch')
+
+    def record_starts(self):
+        """Start of each owner's records in pack()'s buffer (+ the end): owner regions of the key pass."""
+        if self.ocap is None:
+            return np.concatenate([[0], np.cumsum(self.owner_counts)]).astype(np.int64)
+        return np.arange(self.world_x + 1, dtype=np.int64) * self.ocap
 
     def expand_counts(self, nchunk=1):
         """Wait for the expansion; (nchunk, world) records per exchange chunk and owner, raw total."""
@@ -784,6 +812,9 @@ class HipBackend:
         return torch.empty(int(n), dtype=dtype, device=self.device)
 
     def pack(self):
+        if self.ocap is not None:   # the key pass wrote them in place
+            self._chk(self.lib.sbd_pack(self.h, None, None), 'sbd_pack')
+            return self._rec
         n = int(self.owner_counts.sum())
         key = self._empty(n)
         self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), None), 'sbd_pack')

@@ -33,6 +33,8 @@ def _worker(rank, world, port, cfg, outdir):
         os.environ['SB_DIST_CHUNK_MIN'] = '0'
     if 'ck' in cfg:
         os.environ['SB_NOISE_CK'] = str(cfg['ck'])
+    if 'keypass' in cfg:   # 0: the expansion kernel + separate owner partition (sbd_expand_launch) at world > 1
+        os.environ['SB_DIST_KEYPASS'] = str(cfg['keypass'])
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
@@ -77,6 +79,9 @@ CASES = [
     (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'chunks': 2}),
     # owner shards from a 1024-slot table: rebuilt larger between turns (unbounded trail)
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10}),
+    # the legacy expansion (k_expand<true> + stable owner partition) beside the default key pass
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'keypass': 0}),
+    (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3, 'keypass': 0}),
 ]
 
 
