@@ -63,9 +63,8 @@ typedef struct {
                                   (exercises its fallback); bit 4 (test): grow the visited set at 25% projected
                                   load instead of 60% (exercises rebuilds of large tables); bit 5: sharded record
                                   buffers for 48 raw children per parent instead of the worst case (several
-                                  ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY); bit 6: the
-                                  caller expands with sbd_expand_launch_into (no raw-position key buffer is
-                                  preallocated) */
+                                  ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY); bit 6: reserved (set by
+                                  the host when it expands with sbd_expand_parts) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -185,7 +184,10 @@ int sb_debug_topk_scores(int32_t device, const double* scores, int64_t n, int64_
  * the last sb_step), each on a copy of the visited set: out_ms[0] k_expand (one GPU), [1] sharded
  * expansion at world 1, [2] at world 8 (rank 0), [3] world 8 owning no child (every key a record),
  * [4] owner claims of all of [3]'s records, [5] [3] and [4] side by side on two streams, [6] raw count +
- * scan, [7] raw children.  The engine cannot step after this call. */
+ * scan, [7] raw children, [8] the sharded key pass at world 8 (rank 0), [9] its count scan + record move
+ * [10..13] timing-only variants of [8] (no own claims; also a stand-in key; also no stores; no claims and no
+ * stores), [14] k_keys_a owning nothing beside the owner claims of [3]'s records on a second stream
+ * (wall), [15] that k_keys_a alone (out_ms holds 16 floats).  The engine cannot step after this call. */
 int sb_debug_expand_bench(sb_engine* e, int32_t reps, float* out_ms);
 
 /* ---- sharded mode (cfg.world_size > 1 or flags bit 1): per-rank step primitives; the exchanges
@@ -203,14 +205,22 @@ int sbd_goal_table(sb_engine* e, uint32_t* first256);
  * chunk_owner_counts[nchunk][world] = records per chunk and owner, *n_raw = successors generated. */
 int sbd_expand_launch(sb_engine* e, int32_t world);
 int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts, int64_t* n_raw);
-/* The same expansion for world > 1 as one key pass (successors hashed, own ones claimed, every other one
- * written as a record straight into its owner's region of d_rec: owner o's records at [o * ocap, o * ocap +
- * count) in (parent, ordinal) order; no separate partition, sbd_pack is then a no-op).  ocap >= the value
- * sbd_record_capacity returns for the current slice; d_rec holds world * ocap keys (world * ocap < 2^32).
- * sbd_expand_counts returns chunk_owner_counts as for sbd_expand_launch (chunk j = the records of parents
- * [j * n / nchunk, (j + 1) * n / nchunk) in 64-parent units). */
-int sbd_record_capacity(sb_engine* e, int32_t world, int64_t* ocap);
-int sbd_expand_launch_into(sb_engine* e, int32_t world, uint64_t* d_rec, int64_t ocap);
+/* Pipelined expansion for world > 1 (sb_keypass.inc): the slice's successors in nparts (<= 16) exchange parts
+ * of consecutive parents, all enqueued without a host wait.  Each part: successors hashed, the ones this rank
+ * owns claimed in its shard, every other one ranked among its owner's records; a per-part event.  n_global =
+ * the turn's parents over all ranks (bounds what this rank can receive).  The raw count is read with
+ * sbd_raw_total after the caller's next wait.  Then per part: sbd_part_counts waits for it and gives its
+ * records per owner (and the answers this rank may receive this turn, the bound for sbd_owner_begin);
+ * sbd_part_pack writes them to the caller's buffer in owner groups, (parent, ordinal) order within each, on
+ * the claim stream; send_base = the part's first index in the turn's concatenated send buffers (the layout
+ * the answers must come back in for sbd_apply).  Received records claim with answer indices in arrival
+ * order (sbd_owner_claim, on the claim stream, beside the later parts' kernels); sbd_owner_total sets the
+ * turn's received count before sbd_owner_finish. */
+int sbd_expand_parts(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global);
+int sbd_part_counts(sb_engine* e, int32_t part, int64_t* owner_counts, int64_t* recv_capacity);
+int sbd_part_pack(sb_engine* e, int32_t part, uint64_t* d_key, int64_t send_base);
+int sbd_set_claim_stream(sb_engine* e, void* stream);
+int sbd_owner_total(sb_engine* e, int64_t n_total);
 /* world 1 (no records, no exchange to size): go on without waiting for the expansion; *n_raw is read by
  * sbd_raw_total after the caller's next wait on the engine stream (sbd_apply's count). */
 int sbd_expand_defer(sb_engine* e);

@@ -838,13 +838,19 @@ struct Engine {
     uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
     std::vector<int64_t> srcb;            // sharded: first answer index of each source's records this turn
     int64_t pending_host = -1;
-    // sharded key pass (sb_keypass.inc, world > 1): the caller's record buffer (world owner regions of ks_ocap
-    // keys), the chunks' look-back words, per-wave scratch, the (chunk, owner) counts + raw total
-    uint64_t* ks_rec = nullptr;
-    uint64_t ks_ocap = 0;
-    bool ks_turn = false;                 // this turn's expansion ran the key pass
-    DBuf<uint64_t> ks_lb, ks_skey;
-    DBuf<uint32_t> ks_sdr, ks_sown, ks_cc;
+    // sharded key pass (sb_keypass.inc, world > 1, sbd_expand_parts): the slice's children in ks_parts exchange
+    // parts (64-parent chunks [ks_c[j], ks_c[j+1])), enqueued back to back on the engine stream; per raw child
+    // its (owner, move, rank) word; per part its (owner, chunk) table + scan, per-owner counts (pinned mirror),
+    // an event; received records' claims run on s_claim (sbd_set_claim_stream) beside the later parts
+    bool ks_pipe = false;                 // this turn's expansion is the pipelined key pass
+    int ks_parts = 0;
+    int64_t ks_c[17] = {};
+    size_t ks_ccoff[17] = {};
+    hipEvent_t ks_ev[16] = {};
+    uint32_t* h_pc = nullptr;             // pinned: per part, per owner record counts (16 x 64)
+    uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
+    hipStream_t s_claim = nullptr;
+    DBuf<uint32_t> ks_rdr, ks_sown, ks_cc, ks_tot, ks_pc;
     double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
 
@@ -920,7 +926,7 @@ static void preallocate_dist(Engine& E) {
     E.cand.ensure(wl * 3);
     E.lost.ensure(wl * 3);
     if (E.cfg.world_size > 1) {   // record buffers for the worst case: sbd_expand_launch needs no host count
-        if (!(E.cfg.flags & 64)) E.cand_key.ensure(wl * E.rec_per_parent);   // bit 6: key pass, caller's regions
+        E.cand_key.ensure(wl * E.rec_per_parent);
         E.cand_pos.ensure(wl * E.rec_per_parent);
         E.digit.ensure(wl * E.rec_per_parent);
         E.rdsc.ensure(wl * E.rec_per_parent);
@@ -1673,6 +1679,15 @@ void sb_destroy(sb_engine* h) {
     E.part_hist.release();
     E.digit.release();
     E.rdsc.release();
+    if (E.s_claim) (void)hipStreamSynchronize(E.s_claim);
+    E.ks_rdr.release();
+    E.ks_sown.release();
+    E.ks_cc.release();
+    E.ks_tot.release();
+    E.ks_pc.release();
+    if (E.h_pc) (void)hipHostFree(E.h_pc);
+    for (auto& e : E.ks_ev)
+        if (e) (void)hipEventDestroy(e);
     if (E.d_tables) (void)hipFree(E.d_tables);
     if (E.d_small) (void)hipFree(E.d_small);
     if (E.d_nraw) (void)hipFree(E.d_nraw);

@@ -30,6 +30,7 @@ reference backend).  All results are bit-identical to the single-GPU engine and 
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 
@@ -305,7 +306,7 @@ class DistSolve:
         self.max_pts = 0
         self.winner = None                      # (turn, global rank)
         self.counts = []                        # per turn: per-rank slice sizes
-        self.b.expand_launch(self.c.world)      # runs while the host does the turn sync / goal check
+        self.b.expand_launch(self.c.world, 1)   # runs while the host does the turn sync / goal check (the root)
         self.lookahead = True                   # step() launches the next turn's expansion before returning
         self._front_deferred = False            # lookahead was off: the next step() launches it
         self._turn_sync()
@@ -377,7 +378,7 @@ class DistSolve:
         # other owners are partitioned by owner.  Exchange chunks: claims of chunk j overlap chunk j+1's transfer
         C = self.nchunk if st['n_parents'] * 24 >= self.chunk_min else 1
         if self._front_deferred:
-            b.expand_launch(c.world)
+            b.expand_launch(c.world, st['n_parents'])
             self._front_deferred = False
         if c.world == 1 and hasattr(b, 'expand_defer'):
             # one rank: no records, nothing to size, so no wait for the expansion; its raw count comes with
@@ -393,6 +394,8 @@ class DistSolve:
             b.apply_finish(int(all_n[0]))
             self._mark(st, 'dedup_exchange')
             return self._post_dedup(st, all_n, off)
+        if getattr(b, 'parts', 0):
+            return self._dedup_parts(st, off)
         cc, n_raw = b.expand_counts(C)                              # (C, world) records per chunk, owner
         M = c.allgather_array(np.concatenate([cc.ravel(), [n_raw]]))
         st['n_raw'] = int(M[:, -1].sum())
@@ -402,10 +405,7 @@ class DistSolve:
         send_key = b.pack()
         self._mark(st, 'pack')
         mine = Mc[me]                                               # my records per chunk, owner
-        own_sz = mine.sum(axis=0)                                   # my records per owner
-        # owner groups in send_key: contiguous, or the key pass's owner regions (record_starts)
-        rs = b.record_starts() if hasattr(b, 'record_starts') else None
-        ostart = np.concatenate([[0], np.cumsum(own_sz)]) if rs is None else np.asarray(rs, dtype=np.int64)
+        ostart = np.concatenate([[0], np.cumsum(mine.sum(axis=0))])  # owner groups in send_key
         ochunk = np.concatenate([np.zeros((1, c.world), np.int64), np.cumsum(mine, axis=0)])
         from_src = Mc[:, :, me]                                     # [source][chunk] records to me
         src_tot = from_src.sum(axis=1)
@@ -434,6 +434,7 @@ class DistSolve:
         b.owner_finish(ret)
         self._mark(st, 'a2a_keys+claim')
         # answers back to the sources, one bit per answer on the wire (8x less than the answer bytes)
+        own_sz = ostart[1:] - ostart[:-1]
         if c.world > 1:
             nb = lambda x: (int(x) + 7) // 8
             sp = np.concatenate([[0], np.cumsum([nb(src_tot[q]) for q in range(c.world)])])
@@ -448,9 +449,83 @@ class DistSolve:
             back = b.answer_buffer(int(ostart[-1]))
             for o in range(c.world):
                 if own_sz[o]:
-                    b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o] + own_sz[o])])
+                    b.unpack_bits(rbits[int(rp[o]):int(rp[o + 1])], back[int(ostart[o]):int(ostart[o + 1])])
         else:
             back = ret[:0]
+        all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
+        b.apply_finish(int(all_n[c.rank]))
+        self._mark(st, 'dedup_exchange')
+        return self._post_dedup(st, all_n, off)
+
+    def _dedup_parts(self, st, off):
+        """Dedup with the pipelined key pass (b.parts exchange parts of consecutive parents): for each part,
+        its records per owner (one host all_gather of the counts), its keys to their owners (all_to_all), and
+        the owners' claims of them — on the claim stream, beside the next parts' key pass on the engine
+        stream.  Answer indices follow arrival order (part by part, source by source), which within a source
+        is (parent, ordinal) order: the claim tags (turn | source | answer index) order like the reference's
+        first occurrence (src/solver.py:446-450).  Then the answers go back as bits, one all_to_all."""
+        c, b = self.c, self.b
+        me, W, P = c.rank, c.world, b.parts
+        cs = b.claim_stream()
+        ctx = (lambda: torch.cuda.stream(cs)) if cs is not None else contextlib.nullcontext
+        sends, recvs = [], []
+        send_base = ans_base = 0
+        ret = None
+        for j in range(P):
+            cnt, cap = b.part_counts(j)                       # waits for part j's key pass only
+            extra = [b.raw_total()] if j == 0 else []         # the raw count is known before the parts
+            M = c.allgather_array(np.concatenate([cnt, extra]), host=True)
+            if j == 0:
+                st['n_raw'] = int(M[:, W].sum())
+                M = M[:, :W]
+                b.owner_begin(cap, [0] * W)
+                ret = b.answer_buffer(cap)
+                self._mark(st, 'expand')
+            from_src = M[:, me]                               # records each source sends me in this part
+            ostart = np.concatenate([[0], np.cumsum(cnt)])
+            with ctx():
+                key = b.part_pack(j, int(ostart[-1]), send_base)
+                pieces = [key[int(ostart[o]):int(ostart[o + 1])] for o in range(W)]
+                rkey, hd = c.alltoall_pieces(pieces, from_src)
+                c.wait(hd)                                    # RCCL: the claim stream waits for the transfer
+                if rkey.numel():
+                    starts = np.concatenate([[0], np.cumsum(from_src)[:-1]])
+                    b.owner_claim(rkey, starts, ans_base + starts, ret)
+            sends.append((cnt, send_base, ostart))
+            recvs.append((from_src, ans_base))
+            send_base += int(ostart[-1])
+            ans_base += int(from_src.sum())
+        b.owner_total(ans_base)
+        with ctx():
+            b.owner_finish(ret)
+        if cs is not None:
+            torch.cuda.current_stream().wait_stream(cs)
+        self._mark(st, 'a2a_keys+claim')
+        # answers back to the sources as bits: to source q, its (part j) segments in part order
+        nb = lambda x: (int(x) + 7) // 8
+        sp = [0]
+        for q in range(W):
+            sp.append(sp[-1] + sum(nb(fs[q]) for fs, _ in recvs))
+        rp = [0]
+        for o in range(W):
+            rp.append(rp[-1] + sum(nb(cn[o]) for cn, _, _ in sends))
+        sbits = b.answer_buffer(sp[-1])
+        rbits = b.answer_buffer(rp[-1])
+        for q in range(W):
+            at = sp[q]
+            for fs, ab in recvs:
+                a0 = ab + int(np.sum(fs[:q]))
+                if fs[q]:
+                    b.pack_bits(ret[a0:a0 + int(fs[q])], sbits[at:at + nb(fs[q])])
+                at += nb(fs[q])
+        c.alltoall_into([sbits[sp[q]:sp[q + 1]] for q in range(W)], [rbits[rp[o]:rp[o + 1]] for o in range(W)])
+        back = b.answer_buffer(send_base)
+        for o in range(W):
+            at = rp[o]
+            for cn, sb, os_ in sends:
+                if cn[o]:
+                    b.unpack_bits(rbits[at:at + nb(cn[o])], back[sb + int(os_[o]):sb + int(os_[o]) + int(cn[o])])
+                at += nb(cn[o])
         all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
@@ -511,7 +586,7 @@ class DistSolve:
         if self.heur:
             self.noise.background()
         if self.lookahead:
-            b.expand_launch(c.world)   # the next turn's expansion overlaps its goal check
+            b.expand_launch(c.world, K)   # the next turn's expansion (K parents in all) overlaps its goal check
         else:   # a benchmark's window edge (bench.py): the next step() launches it
             self._front_deferred = True
         self._turn_sync()
@@ -641,6 +716,10 @@ class HipBackend:
     it needs a value (counts that size an all_to_all, the goal table).
     """
 
+    # world > 1: the key pass (flags bit 6, sb_keypass.inc) instead of the expansion kernel + owner partition
+    KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'
+    PARTS = int(os.environ.get('SB_DIST_PARTS', '4'))   # exchange parts of the pipelined key pass (<= 16)
+
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
                  heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0,
                  extra_flags: int = 0):
@@ -665,6 +744,12 @@ class HipBackend:
         self.stream = torch.cuda.Stream(self.device)
         torch.cuda.set_stream(self.stream)
         L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
+        # world > 1: the pipelined key pass; received records are claimed on a second stream beside it
+        self.parts = max(1, min(16, self.PARTS)) if (self.KEYPASS and world > 1) else 0
+        self.cstream = None
+        if self.parts:
+            self.cstream = torch.cuda.Stream(self.device)
+            L.check(self.lib.sbd_set_claim_stream(self.h, C.c_void_p(self.cstream.cuda_stream)), 'sbd_set_claim_stream')
 
     def _bind(self):
         C, lib = self.C, self.lib
@@ -675,8 +760,11 @@ class HipBackend:
         lib.sbd_goal_table.argtypes = [vp, vp]
         lib.sbd_expand_launch.argtypes = [vp, i32]
         lib.sbd_expand_counts.argtypes = [vp, i32, vp, p64]
-        lib.sbd_record_capacity.argtypes = [vp, i32, p64]
-        lib.sbd_expand_launch_into.argtypes = [vp, i32, vp, i64]
+        lib.sbd_expand_parts.argtypes = [vp, i32, i32, i64]
+        lib.sbd_part_counts.argtypes = [vp, i32, vp, p64]
+        lib.sbd_part_pack.argtypes = [vp, i32, vp, i64]
+        lib.sbd_set_claim_stream.argtypes = [vp, vp]
+        lib.sbd_owner_total.argtypes = [vp, i64]
         lib.sbd_expand_defer.argtypes = [vp]
         lib.sbd_raw_total.argtypes = [vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
@@ -761,33 +849,35 @@ class HipBackend:
         return self.L.visited_capacity(self.h)
 
     # ---------------------------------------------------------------- step primitives
-    KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'   # world > 1: one key pass writing owner regions
-
-    def expand_launch(self, world):
+    def expand_launch(self, world, n_global=0):
         """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait.
-        world > 1: the key pass (sbd_expand_launch_into) writes the records into owner regions of a
-        buffer held here (record_starts()), so pack() has nothing to do."""
+        world > 1: the pipelined key pass in self.parts exchange parts (n_global: the turn's parents over
+        all ranks, bounds what this rank receives)."""
         self.world_x = int(world)
-        self.ocap = None
-        if world > 1 and self.KEYPASS:
-            C = self.C
-            oc = C.c_int64()
-            self._chk(self.lib.sbd_record_capacity(self.h, int(world), C.byref(oc)), 'sbd_record_capacity')
-            need = int(world) * oc.value
-            if getattr(self, '_rec', None) is None or self._rec.numel() < need:
-                self._rec = None
-                self._rec = self._empty(need + need // 4)   # slack: regrown rarely
-            self.ocap = oc.value
-            self._chk(self.lib.sbd_expand_launch_into(self.h, int(world), self._rec.data_ptr(), oc.value),
-                      'sbd_expand_launch_into')
+        if self.parts and world > 1:
+            self._chk(self.lib.sbd_expand_parts(self.h, int(world), int(self.parts), int(n_global)), 'sbd_expand_parts')
             return
         self._chk(self.lib.sbd_expand_launch(self.h, int(world)), 'sbd_expand_launch')
 
-    def record_starts(self):
-        """Start of each owner's records in pack()'s buffer (+ the end): owner regions of the key pass."""
-        if self.ocap is None:
-            return np.concatenate([[0], np.cumsum(self.owner_counts)]).astype(np.int64)
-        return np.arange(self.world_x + 1, dtype=np.int64) * self.ocap
+    def claim_stream(self):
+        return self.cstream
+
+    def part_counts(self, j):
+        """Part j's records per owner (waits for its key pass) and the turn's receive bound."""
+        C = self.C
+        cnt = np.zeros(self.world_x, np.int64)
+        cap = C.c_int64()
+        self._chk(self.lib.sbd_part_counts(self.h, int(j), cnt.ctypes.data, C.byref(cap)), 'sbd_part_counts')
+        return cnt, cap.value
+
+    def part_pack(self, j, n, send_base):
+        """Part j's n records in owner groups (on the claim stream: the caller's current stream)."""
+        key = self._empty(max(int(n), 1))[:int(n)]
+        self._chk(self.lib.sbd_part_pack(self.h, int(j), key.data_ptr() if n else None, int(send_base)), 'sbd_part_pack')
+        return key
+
+    def owner_total(self, n):
+        self._chk(self.lib.sbd_owner_total(self.h, int(n)), 'sbd_owner_total')
 
     def expand_counts(self, nchunk=1):
         """Wait for the expansion; (nchunk, world) records per exchange chunk and owner, raw total."""
@@ -812,9 +902,6 @@ class HipBackend:
         return torch.empty(int(n), dtype=dtype, device=self.device)
 
     def pack(self):
-        if self.ocap is not None:   # the key pass wrote them in place
-            self._chk(self.lib.sbd_pack(self.h, None, None), 'sbd_pack')
-            return self._rec
         n = int(self.owner_counts.sum())
         key = self._empty(n)
         self._chk(self.lib.sbd_pack(self.h, key.data_ptr(), None), 'sbd_pack')

@@ -46,6 +46,7 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     st = random.getstate()[1]
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
+    b.parts = cfg.get('parts', 0)   # > 0: the pipelined protocol (the HIP key pass's exchange parts)
     comm = Comm(torch.device('cpu'))
     if cfg.get('serialize'):   # the profiling wrappers (bench_dist.py SB_DIST_SERIALIZE=1) change nothing
         from splendor_amd.dist import SerializedBackend
@@ -88,6 +89,15 @@ CASES = [
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True}),
     # the per-rank profiling wrapper (one rank's backend calls at a time) changes no result
     (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'serialize': True}),
+    # the pipelined protocol: records exchanged and claimed part by part, answer-index tags
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3}),
+    (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True, 'parts': 2}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'parts': 2}),
+    (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'parts': 1}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'parts': 4}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'parts': 4}),
+    (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'serialize': True,
+         'parts': 2}),
 ]
 
 

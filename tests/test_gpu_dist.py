@@ -35,6 +35,8 @@ def _worker(rank, world, port, cfg, outdir):
         os.environ['SB_NOISE_CK'] = str(cfg['ck'])
     if 'keypass' in cfg:   # 0: the expansion kernel + separate owner partition (sbd_expand_launch) at world > 1
         os.environ['SB_DIST_KEYPASS'] = str(cfg['keypass'])
+    if 'parts' in cfg:     # exchange parts of the pipelined key pass (default 4)
+        os.environ['SB_DIST_PARTS'] = str(cfg['parts'])
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
@@ -82,6 +84,9 @@ CASES = [
     # the legacy expansion (k_expand<true> + stable owner partition) beside the default key pass
     (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'keypass': 0}),
     (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3, 'keypass': 0}),
+    # the pipelined key pass in one part, and in 16 (parts of a few chunks, some empty on small turns)
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'parts': 1}),
+    (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'parts': 16}),
 ]
 
 
