@@ -187,7 +187,10 @@ int sb_debug_topk_scores(int32_t device, const double* scores, int64_t n, int64_
  * scan, [7] raw children, [8] the sharded key pass at world 8 (rank 0), [9] its count scan + record move
  * [10..13] timing-only variants of [8] (no own claims; also a stand-in key; also no stores; no claims and no
  * stores), [14] k_keys_a owning nothing beside the owner claims of [3]'s records on a second stream
- * (wall), [15] that k_keys_a alone (out_ms holds 16 floats).  The engine cannot step after this call. */
+ * (wall), [15] that k_keys_a alone, [16] one rank's pipelined dedup at world 8 (4 parts: key pass + the claims
+ * of the records standing in for what the other ranks send) on two streams (wall), [17] the same on one
+ * stream, [18] with the key passes on a high-priority stream and the claims on a low-priority one, [19]
+ * the device's stream priority levels (out_ms holds 20 floats).  The engine cannot step after this call. */
 int sb_debug_expand_bench(sb_engine* e, int32_t reps, float* out_ms);
 
 /* ---- sharded mode (cfg.world_size > 1 or flags bit 1): per-rank step primitives; the exchanges

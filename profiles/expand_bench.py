@@ -30,12 +30,13 @@ for t in range(a.turn):
     print(f'turn {t}: parents {st["n_parents"]} unique {st["n_unique"]} kept {st["n_kept"]}', file=sys.stderr, flush=True)
 lib = L.lib()
 lib.sb_debug_expand_bench.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
-out = (C.c_float * 16)()
+out = (C.c_float * 20)()
 L.check(lib.sb_debug_expand_bench(eng._h, a.reps, out), 'sb_debug_expand_bench')
 names = ['expand_fused_1gpu', 'sharded_w1', 'sharded_w8_rank0', 'sharded_w8_no_own', 'claims_all_records',
          'no_own_beside_claims_wall', 'raw_count_scan', 'raw_children', 'keypass_a_w8', 'keypass_scan_b_w8',
          'dbg_a_no_claims', 'dbg_a_no_claims_cheap_key', 'dbg_a_no_claims_key_stores', 'dbg_a_no_claims_no_stores',
-         'keys_a_no_own_beside_claims_wall', 'keys_a_no_own']
+         'keys_a_no_own_beside_claims_wall', 'keys_a_no_own', 'pipelined_dedup_w8_two_streams',
+         'pipelined_dedup_w8_one_stream', 'pipelined_dedup_w8_priority_streams', 'stream_priority_levels']
 res = {k: round(float(v), 4) for k, v in zip(names, out)}
 res.update(turn=a.turn, parents=eng.turn_size(a.turn), width=a.width, heuristic=a.heuristic, reps=a.reps)
 print(json.dumps(res), flush=True)
