@@ -3,7 +3,7 @@
 
 Each rank's kernel trace (rocprofv3 --kernel-trace, one process per rank, SB_DIST_SERIALIZE=1 so every
 kernel ran alone on the device) is cut into steps at its k_expand<true> launches (a step's expansion is
-launched at the end of the previous step; the timed window is the last --steps of them).  Kernels are
+launched at the end of the previous step, its first kernel k_raw_count; the timed window is the last --steps).  Kernels are
 assigned to phases by name, k_part_* by position (before the apply: the owner partition of the records;
 after: the rebalance of the kept records).  Prints a table (ms per step, mean over the timed steps and
 ranks, and the slowest rank) and writes it as JSON with --out.
@@ -16,7 +16,8 @@ import re
 from collections import defaultdict
 
 PHASES = [
-    ('expand', r'^k_expand<true>|^k_keys_sh|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
+    ('expand', r'^k_expand<true>|^k_keys_a|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
+    ('record pack', r'^k_keys_b'),
     ('owner partition', r'^k_part_|^k_chunk_counts'),
     ('owner claims', r'^k_own_'),
     ('answer bits', r'^k_(un)?pack_bits'),
@@ -77,7 +78,7 @@ def rank_table(rows, steps, ovl=None):
             if not o:
                 clean[name].append((t1 - t0) / 1e6)
     med = {k: sorted(v)[len(v) // 2] for k, v in clean.items()}
-    ex = [i for i, r in enumerate(rows) if r[0] in ('k_expand<true>', 'k_keys_sh')]
+    ex = [i for i, r in enumerate(rows) if r[0] == 'k_raw_count']   # each step's expansion starts with it
     if len(ex) < steps:
         raise RuntimeError(f'only {len(ex)} expansions in the trace')
     starts = ex[-steps:] + [len(rows)]
