@@ -245,6 +245,12 @@ int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
  * unpack is the inverse (n answer bytes from ceil(n/8) packed bytes).  Both on the engine stream. */
 int sbd_pack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
 int sbd_unpack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
+/* the same over nseg segments in one launch (device bases + host tables of offsets; len = answer bytes):
+ * pack: bytes d_src[src_off[s], + len[s]) -> bits d_dst[dst_off[s], + ceil(len[s]/8)); unpack the inverse. */
+int sbd_pack_bits_segs(sb_engine* e, const uint8_t* d_src, int32_t nseg, const int64_t* src_off, const int64_t* len,
+                       uint8_t* d_dst, const int64_t* dst_off);
+int sbd_unpack_bits_segs(sb_engine* e, const uint8_t* d_src, int32_t nseg, const int64_t* src_off, const int64_t* len,
+                         uint8_t* d_dst, const int64_t* dst_off);
 /* apply the answers (in pack order): this rank's next_queue entries as an int64 at n_unique_dev (device),
  * without waiting (the caller all-gathers it on the engine stream); sbd_apply_finish(that value) then
  * checks the step's error word and updates the host state. */

@@ -533,6 +533,28 @@ __global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long
         cnt[r] = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
                  __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
 }
+// the same with the scan's first kernel folded in: a block counts one SCAN_TILE tile of parents (strided,
+// coalesced) and stores the tile's sum for scan_exclusive_u32_sums (k_scan_reduce would read cnt again)
+__global__ __launch_bounds__(256) void k_count_lm_tiles(int64_t n, const unsigned long long* __restrict__ cand,
+                                                        const unsigned long long* __restrict__ lost,
+                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ tile_sums) {
+    __shared__ uint32_t lds[256 / 64 + 1];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x;
+    uint32_t s = 0;
+#pragma unroll 4
+    for (int j = 0; j < SCAN_TILE / 256; j++) {
+        const int64_t r = base + (int64_t)j * 256;
+        if (r < n) {
+            const uint32_t c = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
+                               __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
+            cnt[r] = c;
+            s += c;
+        }
+    }
+    uint32_t tot;
+    block_excl_scan<256>(s, lds, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
 
 #include "sb_wave.inc"
 
@@ -947,7 +969,7 @@ static void preallocate_dist(Engine& E) {
     E.part_hist.ensure(dtiles * (size_t)std::max(1, (int)E.cfg.world_size) + 80 + 16 * 64);
     E.kidx.ensure(wl);
     E.rkey.ensure(wl);
-    topk_reserve(E.topk, (int64_t)nu, (int64_t)wl);
+    topk_reserve(E.topk, (int64_t)wl, (int64_t)wl);   // the receive sort only (the joint select is k_ds_*)
     E.scan.tiles.ensure(nr / SCAN_TILE + 1);
     E.turn_mem.reserve(wl * 20 * 24);
 }
@@ -1017,10 +1039,14 @@ static void launch_front(Engine& E) {
                            (uint8_t*)nullptr);
     }
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
-    if (n > 0)
-        hipLaunchKernelGGL(k_count_lm, dim3(grid_cap(n, 256, 1u << 14)), dim3(256), 0, E.s, n, E.cand.p, E.lost.p,
-                           E.cnt.p);
-    scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
+    if (n > 0) {   // survivors per parent + their tile sums, then the offsets (next_queue order)
+        E.scan.tiles.ensure((size_t)((n + SCAN_TILE - 1) / SCAN_TILE));
+        hipLaunchKernelGGL(k_count_lm_tiles, dim3((unsigned)((n + SCAN_TILE - 1) / SCAN_TILE)), dim3(256), 0, E.s, n,
+                           E.cand.p, E.lost.p, E.cnt.p, E.scan.tiles.p);
+        scan_exclusive_u32_sums(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
+    } else {
+        scan_exclusive_u32(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
+    }
     if (timing) SB_HIP(hipEventRecord(ev[2], E.s));
     SB_HIP(hipMemcpyAsync(E.h_small, E.d_small, 264 * 4, hipMemcpyDeviceToHost, E.s));
     SB_HIP(hipMemcpyAsync(E.h_nraw, E.d_nraw, 8, hipMemcpyDeviceToHost, E.s));

@@ -85,11 +85,14 @@ struct ScanScratch {
     DBuf<uint32_t> tiles;
 };
 constexpr int SCAN_TILE = 4096;
-// exclusive scan of n u32 values (in may equal out); *total_dev (u32, device) receives the sum
 // single-workgroup exclusive scan of a short array in place (tile sums); *total_dev gets the sum
 void scan_tiles_inplace(uint32_t* tiles, int64_t ntiles, uint32_t* total_dev, hipStream_t st);
+// exclusive scan of n u32 values (in may equal out); *total_dev (u32, device) receives the sum
 void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev, ScanScratch& s,
                         hipStream_t st);
+// the same when the caller's kernel already wrote the SCAN_TILE tile sums into s.tiles (n > 0)
+void scan_exclusive_u32_sums(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev, ScanScratch& s,
+                             hipStream_t st);
 
 // ---- stable top-k (sb_sort.hip) ----
 struct TopkScratch {
@@ -104,6 +107,8 @@ struct TopkScratch {
     DBuf<uint32_t> fx_mark;         // sort fix-up: run claims (epoch stamps)
     DBuf<uint32_t> osh_part;        // sort digit histograms: one row per k_os_hist block (two-stage flush)
     DBuf<uint32_t> tkh_part;        // select histograms: one row per k_tk_hist block (two-stage flush)
+    DBuf<uint64_t> sk;              // select: staged first-partition keys (one TK_TILE region per tile)
+    DBuf<uint32_t> si;              // select: staged first-partition payloads
     uint32_t fx_epoch = 0;
     void release();
 };

@@ -53,6 +53,10 @@ constexpr int64_t TK_WRITE_GRID = SB_TK_WRITE_GRID;           // candidate passe
 #define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
 #endif
 constexpr int OS_PREFIX_BITS = SB_SORT_PREFIX_BITS;
+#ifndef SB_TK_STAGE
+#define SB_TK_STAGE 1            // first partition: one read, staged per tile (0: count + write, two reads)
+#endif
+constexpr bool TK_STAGE = SB_TK_STAGE;
 
 
 // device state (u64 words)
@@ -71,6 +75,7 @@ enum : int {
     ST_SH32,    // sort: low bits below the sorted 40-bit prefix
     ST_FXN,     // fix-up: flagged positions (prefix equal to the predecessor's, key not)
     ST_FXI,     // fix-up: work counter over the flagged positions
+    ST_HARR,    // select histogram: blocks arrived (the last one picks: SB_TK_PICK_FUSED)
     ST_HIST = 20,
     ST_WORDS = ST_HIST + SEL_BINS
 };
@@ -142,15 +147,70 @@ __device__ __forceinline__ void tk_setup_body(uint64_t* st) {
 }
 __global__ void k_tk_setup(uint64_t* st) { tk_setup_body(st); }
 
+// pick the bucket holding the need-th largest matching element; clears the histogram.  NT threads;
+// AT: read the histogram with agent-scope loads (the last block of k_tk_hist, whose flushes came from
+// other blocks of the same launch)
+template <int NT, bool AT>
+__device__ __forceinline__ void tk_pick_body(uint64_t* st) {
+    __shared__ uint32_t lds[NT / 64 + 1];
+    const int t = threadIdx.x;
+    const uint64_t sh = st[ST_SH];
+    const uint64_t d = sh < SEL_D ? sh : SEL_D;
+    const int nb = 1 << d;
+    constexpr int PER = SEL_BINS / NT;   // bins per thread, descending
+    uint64_t c[PER];
+    uint64_t loc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int b = nb - 1 - (t * PER + j);
+        c[j] = b < 0 ? 0ull
+                     : AT ? (uint64_t)__hip_atomic_load((unsigned long long*)&st[ST_HIST + b], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                          : st[ST_HIST + b];
+        loc += c[j];
+    }
+    // counts fit in u32 (n < 2^32)
+    uint32_t tot;
+    uint64_t cum = block_excl_scan<NT>((uint32_t)loc, lds, &tot);
+    const uint64_t need = st[ST_NEED];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int b = nb - 1 - (t * PER + j);
+        if (b >= 0 && c[j] && cum < need && cum + c[j] >= need) {
+            const uint64_t nneed = need - cum;
+            st[ST_NEED] = nneed;
+            st[ST_PREFIX] = (st[ST_PREFIX] << d) | (uint64_t)b;
+            st[ST_SH] = sh - d;
+            st[ST_DONE] = (c[j] == nneed) || (sh - d == 0);
+        }
+        cum += c[j];
+    }
+    for (int b = t; b < SEL_BINS; b += NT) st[ST_HIST + b] = 0;
+}
+
+#ifndef SB_TK_PICK_FUSED
+#define SB_TK_PICK_FUSED 0   // 1: the select histogram's last block picks (no k_tk_pick launch per pass).  A/B
+                             // (profiles/r3/s5/ab_topk.txt): every block's agent-scope release fence writes its
+                             // XCD's L2 back: k_tk_hist 109 -> 421 us per step, select 0.61 -> 0.90 ms
+#endif
+
 // histogram of the next digit over the elements matching the resolved prefix; n from n_dev if given
 // part != nullptr: the block stores its row of SEL_BINS counts there (k_tk_hsum adds the rows up)
-__global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
+#ifndef SB_TKH_NT
+#define SB_TKH_NT 1024     // threads per select-histogram block: 4x the resident waves of 256 at the same flush
+                           // count (prepass 89 -> 77 us, profiles/r3/s5/ab_topk.txt)
+#endif
+constexpr int TKH_NT = SB_TKH_NT;
+constexpr int TKH_NH = TKH_NT / 64 < 4 ? TKH_NT / 64 : 4;   // LDS sub-histograms (waves share them beyond 4)
+__global__ __launch_bounds__(TKH_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
                                                    const uint64_t* __restrict__ n_dev, uint64_t* st, int only_fallback,
-                                                   uint32_t* __restrict__ part) {
+                                                   uint32_t* __restrict__ part, int pick) {
     if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
-    __shared__ uint32_t h[TK_NT / 64][SEL_BINS];
-    const int w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < (TK_NT / 64) * SEL_BINS; i += TK_NT) (&h[0][0])[i] = 0;
+    __shared__ uint32_t h[TKH_NH][SEL_BINS];
+    __shared__ int s_last;
+    const int w = (threadIdx.x >> 6) % TKH_NH;
+    for (int i = threadIdx.x; i < TKH_NH * SEL_BINS; i += TKH_NT) (&h[0][0])[i] = 0;
     __syncthreads();
     const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
     const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
@@ -158,8 +218,8 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
     const uint64_t dmask = (1ull << d) - 1;
     const uint64_t lt = lanemask_lt();
     constexpr int U = SB_TKH_U;   // loads in flight per thread
-    const int64_t stride = (int64_t)gridDim.x * TK_NT;
-    for (int64_t i0 = (int64_t)blockIdx.x * TK_NT + threadIdx.x; i0 < n; i0 += stride * U) {
+    const int64_t stride = (int64_t)gridDim.x * TKH_NT;
+    for (int64_t i0 = (int64_t)blockIdx.x * TKH_NT + threadIdx.x; i0 < n; i0 += stride * U) {
         uint64_t kk[U];
 #pragma unroll
         for (int u = 0; u < U; u++) kk[u] = i0 + u * stride < n ? keys[i0 + u * stride] : 0ull;
@@ -181,10 +241,24 @@ __global__ __launch_bounds__(TK_NT) void k_tk_hist(const uint64_t* __restrict__ 
         }
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < SEL_BINS; b += TK_NT) {
-        const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
+    for (int b = threadIdx.x; b < SEL_BINS; b += TKH_NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int x = 0; x < TKH_NH; x++) c += h[x][b];
         if (part) part[(size_t)blockIdx.x * SEL_BINS + b] = c;
         else if (c) atomicAdd((unsigned long long*)&st[ST_HIST + b], (unsigned long long)c);
+    }
+    if (pick) {   // the last block to arrive picks: every block's flush is performed before its arrival
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_last = atomicAdd((unsigned long long*)&st[ST_HARR], 1ull) == (unsigned long long)gridDim.x - 1;
+        __syncthreads();
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            tk_pick_body<TKH_NT, true>(st);
+            if (threadIdx.x == 0) st[ST_HARR] = 0;
+        }
     }
 }
 // column sums of k_tk_hist's rows: grid (SEL_BINS / 256, ceil(rows / 32)), thread = bin; one atomic
@@ -203,54 +277,26 @@ __global__ __launch_bounds__(256) void k_tk_hsum(const uint32_t* __restrict__ pa
 #ifndef SB_TKH_2STAGE
 #define SB_TKH_2STAGE 0   // A/B: select +40 us (profiles/r2_ab_hist_flush.txt)
 #endif
-static void tk_hist(TopkScratch& s, hipStream_t st, const uint64_t* keys, int64_t n, const uint64_t* n_dev,
-                    uint64_t* stv, int only_fallback, unsigned grid) {
+__global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallback);
+// one select pass: the histogram of the next digit, then the pick (in the histogram's last block, or a launch)
+static void tk_hist_pick(TopkScratch& s, hipStream_t st, const uint64_t* keys, int64_t n, const uint64_t* n_dev,
+                         uint64_t* stv, int only_fallback, unsigned grid) {
     uint32_t* part = nullptr;
     if (SB_TKH_2STAGE) {
         s.tkh_part.ensure((size_t)grid * SEL_BINS);
         part = s.tkh_part.p;
     }
-    hipLaunchKernelGGL(k_tk_hist, dim3(grid), dim3(TK_NT), 0, st, keys, n, n_dev, stv, only_fallback, part);
+    const int fused_pick = SB_TK_PICK_FUSED && !part;
+    hipLaunchKernelGGL(k_tk_hist, dim3(grid), dim3(TKH_NT), 0, st, keys, n, n_dev, stv, only_fallback, part, fused_pick);
     if (part)
         hipLaunchKernelGGL(k_tk_hsum, dim3(SEL_BINS / 256, (grid + 31) / 32), dim3(256), 0, st, part, (int)grid, stv,
                            only_fallback);
+    if (!fused_pick) hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, only_fallback);
 }
 
-// pick the bucket holding the need-th largest matching element; clears the histogram
 __global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallback) {
     if (st[ST_DONE] || (only_fallback && !st[ST_FALLBACK])) return;
-    __shared__ uint32_t lds[TK_NT / 64 + 1];
-    const int t = threadIdx.x;
-    const uint64_t sh = st[ST_SH];
-    const uint64_t d = sh < SEL_D ? sh : SEL_D;
-    const int nb = 1 << d;
-    constexpr int PER = SEL_BINS / TK_NT;   // 8 bins per thread, descending
-    uint64_t c[PER];
-    uint64_t loc = 0;
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int b = nb - 1 - (t * PER + j);
-        c[j] = b >= 0 ? st[ST_HIST + b] : 0;
-        loc += c[j];
-    }
-    // counts fit in u32 (n < 2^32)
-    uint32_t tot;
-    uint64_t cum = block_excl_scan<TK_NT>((uint32_t)loc, lds, &tot);
-    const uint64_t need = st[ST_NEED];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int b = nb - 1 - (t * PER + j);
-        if (b >= 0 && c[j] && cum < need && cum + c[j] >= need) {
-            const uint64_t nneed = need - cum;
-            st[ST_NEED] = nneed;
-            st[ST_PREFIX] = (st[ST_PREFIX] << d) | (uint64_t)b;
-            st[ST_SH] = sh - d;
-            st[ST_DONE] = (c[j] == nneed) || (sh - d == 0);
-        }
-        cum += c[j];
-    }
-    for (int b = t; b < SEL_BINS; b += TK_NT) st[ST_HIST + b] = 0;
+    tk_pick_body<TK_NT, false>(st);
 }
 
 // First pass from the histogram the emission folded (bins of key >> 47 in [FBASE, FBASE + 2048), the
@@ -432,6 +478,14 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
             const uint64_t bg = __ballot(g), be = __ballot(e);
             if (l == 0) cnt[r * NW + w] = (uint32_t)__popcll(bg) | ((uint32_t)__popcll(be) << 16);
         }
+        // the written elements' payloads, all loads in flight across the barriers (loaded in the write loop,
+        // each round waited for its own load: up to 16 latencies per tile)
+        uint32_t pv[TK_IPT];
+#pragma unroll
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            pv[r] = ((fg | fe) >> r) & 1 ? (idx ? idx[i] : (pay ? pay[i] : (uint32_t)i)) : 0u;
+        }
         __syncthreads();
         if (t < 64) {   // exclusive scan of the 64 packed counts (round-major = index order)
             const uint32_t v = t < TK_IPT * NW ? cnt[t] : 0u;
@@ -445,22 +499,137 @@ __global__ __launch_bounds__(TK_NT) void k_tk_write(const uint64_t* __restrict__
 #pragma unroll
             for (int r = 0; r < TK_IPT; r++) {
                 const uint64_t bg = __ballot((fg >> r) & 1), be = __ballot((fe >> r) & 1);
-                const int64_t i = base + (int64_t)r * TK_NT + t;
                 const uint32_t c = cnt[r * NW + w];
                 if ((fg >> r) & 1) {
                     const uint64_t o = og + (c & 0xFFFFu) + __popcll(bg & lt);
                     gk[o] = kk[r];
-                    gi[o] = idx ? idx[i] : (pay ? pay[i] : (uint32_t)i);
+                    gi[o] = pv[r];
                 } else if ((fe >> r) & 1) {
                     const uint64_t re = oe + (c >> 16) + __popcll(be & lt);
                     if (re < lim) {
                         ek[eb + re] = kk[r];
-                        ei[eb + re] = idx ? idx[i] : (pay ? pay[i] : (uint32_t)i);
+                        ei[eb + re] = pv[r];
                     }
                 }
             }
         }
         __syncthreads();   // the next tile rewrites cnt
+    }
+}
+
+// The first partition over all n keys in one read (SB_TK_STAGE): a tile ranks its elements as k_tk_write
+// does and stages them in its own TK_TILE-slot region of (sk, si) — elements above the prefix from the
+// region's front, equal ones from its back (reversed) — and stores its two counts; k_tk_scan then gives
+// every tile its offsets and k_tk_unstage copies the staged elements to their places.  k_tk_count +
+// k_tk_write read the n keys twice; this reads them once and moves only the staged ~10%.
+__global__ __launch_bounds__(TK_NT) void k_tk_stage(const uint64_t* __restrict__ keys, int64_t n,
+                                                    const uint64_t* __restrict__ st, uint32_t* __restrict__ gt,
+                                                    uint32_t* __restrict__ eq, uint64_t* __restrict__ sk,
+                                                    uint32_t* __restrict__ si, const uint32_t* __restrict__ pay) {
+    constexpr int NW = TK_NT / 64;
+    __shared__ uint32_t cnt[TK_IPT * NW];   // (round, wave): above | equal << 16, then exclusive offsets
+    __shared__ uint32_t tot;
+    const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const uint64_t sh = st[ST_SH], prefix = st[ST_PREFIX];
+    const uint64_t lt = lanemask_lt();
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t base = tile * TK_TILE;
+        uint64_t kk[TK_IPT];
+#pragma unroll
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            kk[r] = i < n ? keys[i] : 0ull;
+        }
+        uint32_t fg = 0, fe = 0;
+#pragma unroll
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            const uint64_t hb = hi_bits(kk[r], sh);
+            const bool g = i < n && hb > prefix, e = i < n && hb == prefix;
+            fg |= (uint32_t)g << r;
+            fe |= (uint32_t)e << r;
+            const uint64_t bg = __ballot(g), be = __ballot(e);
+            if (l == 0) cnt[r * NW + w] = (uint32_t)__popcll(bg) | ((uint32_t)__popcll(be) << 16);
+        }
+        uint32_t pv[TK_IPT];   // payloads of the staged elements, loads in flight across the barriers
+#pragma unroll
+        for (int r = 0; r < TK_IPT; r++) {
+            const int64_t i = base + (int64_t)r * TK_NT + t;
+            pv[r] = ((fg | fe) >> r) & 1 ? (pay ? pay[i] : (uint32_t)i) : 0u;
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t v = t < TK_IPT * NW ? cnt[t] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (t < TK_IPT * NW) cnt[t] = inc - v;
+            if (t == 63) tot = inc;
+        }
+        __syncthreads();
+        if (t == 0) {
+            gt[tile] = tot & 0xFFFFu;
+            eq[tile] = tot >> 16;
+        }
+        if (fg | fe) {
+#pragma unroll
+            for (int r = 0; r < TK_IPT; r++) {
+                const uint64_t bg = __ballot((fg >> r) & 1), be = __ballot((fe >> r) & 1);
+                const uint32_t c = cnt[r * NW + w];
+                int64_t o = -1;
+                if ((fg >> r) & 1) o = base + (c & 0xFFFFu) + __popcll(bg & lt);
+                else if ((fe >> r) & 1) o = base + TK_TILE - 1 - ((c >> 16) + __popcll(be & lt));
+                if (o >= 0) {
+                    sk[o] = kk[r];
+                    si[o] = pv[r];
+                }
+            }
+        }
+        __syncthreads();   // the next tile rewrites cnt
+    }
+}
+
+// staged elements to their places: tile t's above ones to (gk, gi)[gt_off[t] ..), its equal ones (in index
+// order) to (ek, ei)[eq_off[t] ..); counts from consecutive offsets (the last tile's from the totals).  A
+// wave per tile.
+__global__ __launch_bounds__(256) void k_tk_unstage(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ si,
+                                                    int64_t n, const uint64_t* __restrict__ st,
+                                                    const uint32_t* __restrict__ gt_off, const uint32_t* __restrict__ eq_off,
+                                                    uint64_t* __restrict__ gk, uint32_t* __restrict__ gi,
+                                                    uint64_t* __restrict__ ek, uint32_t* __restrict__ ei) {
+    const int64_t ntiles = (n + TK_TILE - 1) / TK_TILE;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t ta = (uint32_t)st[ST_A], te = (uint32_t)st[ST_NC];
+    for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < ntiles; tile += nw) {
+        const uint32_t og = gt_off[tile], oe = eq_off[tile];
+        const uint32_t a = (tile + 1 < ntiles ? gt_off[tile + 1] : ta) - og;
+        const uint32_t e = (tile + 1 < ntiles ? eq_off[tile + 1] : te) - oe;
+        const int64_t base = tile * TK_TILE;
+        constexpr int U = 8;   // loads in flight per lane before the stores
+        for (uint32_t j0 = 0; j0 < a; j0 += 64 * U) {
+            uint64_t kv[U];
+            uint32_t iv[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t j = j0 + u * 64 + lane;
+                if (j < a) {
+                    kv[u] = sk[base + j];
+                    iv[u] = si[base + j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t j = j0 + u * 64 + lane;
+                if (j < a) {
+                    gk[og + j] = kv[u];
+                    gi[og + j] = iv[u];
+                }
+            }
+        }
+        for (uint32_t j = lane; j < e; j += 64) {
+            ek[oe + j] = sk[base + TK_TILE - 1 - j];
+            ei[oe + j] = si[base + TK_TILE - 1 - j];
+        }
     }
 }
 
@@ -536,12 +705,17 @@ __device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64
 // histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
 // cluster); 16 loads in flight per thread
 #ifndef SB_OSH_GRID
-#define SB_OSH_GRID 1024     // 4 blocks per CU: LDS atomic latency hidden (256: 1 per CU, 2x slower)
+#define SB_OSH_GRID 256      // 1024-thread blocks, one per CU (a quarter of the 256-thread grid's flush atomics:
+                             // 39 -> 29 us, profiles/r3/s5/ab_topk.txt)
 #endif
+#ifndef SB_OSH_NT
+#define SB_OSH_NT 1024       // threads per k_os_hist block
+#endif
+constexpr int OSH_NT = SB_OSH_NT;
 #ifndef SB_OSH_WH
 #define SB_OSH_WH 1          // per-wave sub-histograms (less LDS atomic contention between waves)
 #endif
-constexpr int OSH_NH = SB_OSH_WH ? OS_NT / 64 : 1;
+constexpr int OSH_NH = SB_OSH_WH ? (OSH_NT / 64 < 8 ? OSH_NT / 64 : 8) : 1;   // at most 8 (64 KB of LDS)
 // Flush of the blocks' histograms: one atomic per (block, bin).  The two-stage flush (SB_OSH_2STAGE:
 // each block stores its row of P*256 counts, k_os_hsum adds 32 rows per thread with one atomic per
 // (column, 32 rows)) was measured no faster: the same-address atomics are not what bounds k_os_hist.
@@ -550,18 +724,20 @@ constexpr int OSH_NH = SB_OSH_WH ? OS_NT / 64 : 1;
 #endif
 constexpr int OSH_ROW = 8 * 256;     // u32 per block row (digits 0..7)
 constexpr int OSH_RCHUNK = 32;       // rows per k_os_hsum thread
-__global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
-                                                   const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
-                                                   uint32_t* __restrict__ part) {
+// first_dev (optional): count only keys[*first_dev ..) (the rest were counted where they were written)
+__global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
+                                                    const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
+                                                    uint32_t* __restrict__ part, const uint64_t* __restrict__ first_dev) {
     __shared__ uint32_t hh[OSH_NH][8][256];
     const int P = sort_passes(st);
     const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
-    for (int i = threadIdx.x; i < OSH_NH * 8 * 256; i += OS_NT) (&hh[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < OSH_NH * 8 * 256; i += OSH_NT) (&hh[0][0][0])[i] = 0;
     __syncthreads();
-    uint32_t (*h)[256] = hh[SB_OSH_WH ? (threadIdx.x >> 6) : 0];
+    uint32_t (*h)[256] = hh[SB_OSH_WH ? ((threadIdx.x >> 6) % OSH_NH) : 0];
     const uint64_t lt = lanemask_lt();
-    const int64_t stride = (int64_t)gridDim.x * OS_NT;
-    for (int64_t i0 = (int64_t)blockIdx.x * OS_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
+    const int64_t stride = (int64_t)gridDim.x * OSH_NT;
+    const int64_t i_lo = first_dev ? (int64_t)*first_dev : 0;
+    for (int64_t i0 = i_lo + (int64_t)blockIdx.x * OSH_NT + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * OS_IPT) {
         uint64_t kk[OS_IPT];
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) kk[r] = i0 + r * stride < n ? ~sort_prefix(keys[i0 + r * stride], slo, sh) : 0ull;
@@ -584,7 +760,7 @@ __global__ __launch_bounds__(OS_NT) void k_os_hist(const uint64_t* __restrict__ 
     }
     __syncthreads();
     uint32_t* gh = reinterpret_cast<uint32_t*>(lb);
-    for (int i = threadIdx.x; i < P * 256; i += OS_NT) {
+    for (int i = threadIdx.x; i < P * 256; i += OSH_NT) {
         uint32_t c = 0;
 #pragma unroll
         for (int v = 0; v < OSH_NH; v++) c += (&hh[v][0][0])[i];
@@ -930,6 +1106,8 @@ void TopkScratch::release() {
     fx_mark.release();
     osh_part.release();
     tkh_part.release();
+    sk.release();
+    si.release();
 }
 
 // before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
@@ -958,6 +1136,10 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     s.ci.ensure(n);
     s.tile_a.ensure(n / TK_TILE + 1);
     s.tile_b.ensure(n / TK_TILE + 1);
+    if (TK_STAGE && n > keep) {
+        s.sk.ensure((size_t)(n / TK_TILE + 1) * TK_TILE);
+        s.si.ensure((size_t)(n / TK_TILE + 1) * TK_TILE);
+    }
     s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * 256);
     s.small.ensure(ST_WORDS);
     s.fx_list.ensure((size_t)m);
@@ -1009,30 +1191,37 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         const unsigned hg = grid_for(n, TK_NT * 16, SB_TKH_GRID);
         // first digit over all keys (folded into the producer when fused, generic pass as fallback),
         // then partition: above -> output group 1, bucket -> candidates
-        tk_hist(s, st, keys, n, nullptr, stv, (int)fused, hg);
-        hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, (int)fused);
+        tk_hist_pick(s, st, keys, n, nullptr, stv, (int)fused, hg);
         // more digits over all keys before the partition: the scores crowd into few first-pass bins (about
         // half of C3's keys share the threshold's), so the partition would copy most keys as candidates
         for (int e = 0; e < SEL_PREPASS; e++) {
-            tk_hist(s, st, keys, n, nullptr, stv, 0, hg);
-            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
+            tk_hist_pick(s, st, keys, n, nullptr, stv, 0, hg);
         }
         const unsigned cg = (unsigned)std::min<int64_t>(ntiles, TK_COUNT_GRID);
         const unsigned wg = (unsigned)std::min<int64_t>(ntiles, TK_WRITE_GRID);
-        hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
-                           stv, s.tile_a.p, s.tile_b.p);
-        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, (const uint64_t*)nullptr,
-                           stv, (int)ST_A,
-                           (int)ST_NC, 0);
-        hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, keys, (const uint32_t*)nullptr, n,
-                           (const uint64_t*)nullptr, stv, s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p,
-                           (const uint64_t*)nullptr, s.ck.p, s.ci.p, (const uint64_t*)nullptr,
-                           (const uint64_t*)nullptr, payload);
+        if (TK_STAGE) {   // one read of the keys: staged per tile, then moved (k_tk_stage)
+            s.sk.ensure((size_t)ntiles * TK_TILE);
+            s.si.ensure((size_t)ntiles * TK_TILE);
+            hipLaunchKernelGGL(k_tk_stage, dim3(cg), dim3(TK_NT), 0, st, keys, n, stv, s.tile_a.p, s.tile_b.p, s.sk.p,
+                               s.si.p, payload);
+            hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, (const uint64_t*)nullptr,
+                               stv, (int)ST_A, (int)ST_NC, 0);
+            hipLaunchKernelGGL(k_tk_unstage, dim3((unsigned)std::min<int64_t>((ntiles + 3) / 4, 8192)), dim3(256), 0, st,
+                               s.sk.p, s.si.p, n, stv, s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, s.ck.p, s.ci.p);
+        } else {
+            hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, keys, n, (const uint64_t*)nullptr,
+                               stv, s.tile_a.p, s.tile_b.p);
+            hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, (const uint64_t*)nullptr,
+                               stv, (int)ST_A, (int)ST_NC, 0);
+            hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, keys, (const uint32_t*)nullptr, n,
+                               (const uint64_t*)nullptr, stv, s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p,
+                               (const uint64_t*)nullptr, s.ck.p, s.ci.p, (const uint64_t*)nullptr,
+                               (const uint64_t*)nullptr, payload);
+        }
         // remaining digits on the candidates (device-side count; passes after DONE exit at once)
         const uint64_t* nc = stv + ST_NC;
         for (int pass = 0; pass < SEL_PASSES_C; pass++) {
-            tk_hist(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, 512u));
-            hipLaunchKernelGGL(k_tk_pick, dim3(1), dim3(TK_NT), 0, st, stv, 0);
+            tk_hist_pick(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, 512u));
         }
         // candidates above T -> group 2, the first NEED ties -> group 3
         hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
@@ -1052,9 +1241,10 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
     s.os.ensure(lb_words);
     SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
-    const unsigned ohg = grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID);
+    const unsigned ohg = grid_for(m, OSH_NT * OS_IPT, SB_OSH_GRID);
     if (SB_OSH_2STAGE) s.osh_part.ensure((size_t)ohg * OSH_ROW);
-    hipLaunchKernelGGL(k_os_hist, dim3(ohg), dim3(OS_NT), 0, st, s.k0.p, m, stv, s.os.p, s.osh_part.p);
+    hipLaunchKernelGGL(k_os_hist, dim3(ohg), dim3(OSH_NT), 0, st, s.k0.p, m, stv, s.os.p, s.osh_part.p,
+                       (const uint64_t*)nullptr);
     if (SB_OSH_2STAGE)
         hipLaunchKernelGGL(k_os_hsum, dim3(8, (ohg + OSH_RCHUNK - 1) / OSH_RCHUNK), dim3(256), 0, st, s.osh_part.p,
                            (int)ohg, stv, s.os.p);

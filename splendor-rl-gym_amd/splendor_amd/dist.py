@@ -511,21 +511,22 @@ class DistSolve:
             rp.append(rp[-1] + sum(nb(cn[o]) for cn, _, _ in sends))
         sbits = b.answer_buffer(sp[-1])
         rbits = b.answer_buffer(rp[-1])
+        segs = []   # (answer offset, answers, bit-byte offset): every (source, part) segment in one launch
         for q in range(W):
             at = sp[q]
             for fs, ab in recvs:
-                a0 = ab + int(np.sum(fs[:q]))
-                if fs[q]:
-                    b.pack_bits(ret[a0:a0 + int(fs[q])], sbits[at:at + nb(fs[q])])
+                segs.append((ab + int(np.sum(fs[:q])), int(fs[q]), at))
                 at += nb(fs[q])
+        b.pack_bits_segs(ret, segs, sbits)
         c.alltoall_into([sbits[sp[q]:sp[q + 1]] for q in range(W)], [rbits[rp[o]:rp[o + 1]] for o in range(W)])
         back = b.answer_buffer(send_base)
+        segs = []
         for o in range(W):
             at = rp[o]
             for cn, sb, os_ in sends:
-                if cn[o]:
-                    b.unpack_bits(rbits[at:at + nb(cn[o])], back[sb + int(os_[o]):sb + int(os_[o]) + int(cn[o])])
+                segs.append((at, int(cn[o]), sb + int(os_[o])))
                 at += nb(cn[o])
+        b.unpack_bits_segs(rbits, segs, back)
         all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
@@ -773,6 +774,8 @@ class HipBackend:
         lib.sbd_owner_finish.argtypes = [vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_unpack_bits.argtypes = [vp, vp, i64, vp]
+        lib.sbd_pack_bits_segs.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        lib.sbd_unpack_bits_segs.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         lib.sbd_apply.argtypes = [vp, vp, vp]
         lib.sbd_apply_finish.argtypes = [vp, i64]
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
@@ -931,6 +934,23 @@ class HipBackend:
     def unpack_bits(self, src, dst):
         if dst.numel():
             self._chk(self.lib.sbd_unpack_bits(self.h, src.data_ptr(), dst.numel(), dst.data_ptr()), 'sbd_unpack_bits')
+
+    def _bits_segs(self, fn, src, segs, dst):
+        segs = [x for x in segs if x[1] > 0]
+        if not segs:
+            return
+        so, ln, do = (np.ascontiguousarray([x[i] for x in segs], dtype=np.int64) for i in range(3))
+        self._chk(fn(self.h, src.data_ptr(), len(segs), so.ctypes.data, ln.ctypes.data, dst.data_ptr(), do.ctypes.data),
+                  fn.__name__)
+
+    def pack_bits_segs(self, src, segs, dst):
+        """For every (src offset, n, dst offset) in segs: the n answer bytes at src + offset as bits at dst +
+        offset (k_bits_segs: all segments in one launch)."""
+        self._bits_segs(self.lib.sbd_pack_bits_segs, src, segs, dst)
+
+    def unpack_bits_segs(self, src, segs, dst):
+        """The inverse: (src bit-byte offset, n answer bytes, dst offset) per segment, one launch."""
+        self._bits_segs(self.lib.sbd_unpack_bits_segs, src, segs, dst)
 
     def apply(self, back):
         """Survivor masks from the answers; this rank's unique count as a device int64 (no wait)."""
