@@ -534,16 +534,18 @@ __global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long
                  __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
 }
 // the same with the scan's first kernel folded in: a block counts one SCAN_TILE tile of parents (strided,
-// coalesced) and stores the tile's sum for scan_exclusive_u32_sums (k_scan_reduce would read cnt again)
-__global__ __launch_bounds__(256) void k_count_lm_tiles(int64_t n, const unsigned long long* __restrict__ cand,
-                                                        const unsigned long long* __restrict__ lost,
-                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ tile_sums) {
-    __shared__ uint32_t lds[256 / 64 + 1];
+// coalesced) and stores the tile's sum for scan_exclusive_u32_sums (k_scan_reduce would read cnt again).
+// (1024 threads with every mask load issued first measured slower: 52-60 against 43-47 us)
+constexpr int CLT_NT = 256;
+__global__ __launch_bounds__(CLT_NT) void k_count_lm_tiles(int64_t n, const unsigned long long* __restrict__ cand,
+                                                           const unsigned long long* __restrict__ lost,
+                                                           uint32_t* __restrict__ cnt, uint32_t* __restrict__ tile_sums) {
+    __shared__ uint32_t lds[CLT_NT / 64 + 1];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x;
     uint32_t s = 0;
 #pragma unroll 4
-    for (int j = 0; j < SCAN_TILE / 256; j++) {
-        const int64_t r = base + (int64_t)j * 256;
+    for (int j = 0; j < SCAN_TILE / CLT_NT; j++) {
+        const int64_t r = base + (int64_t)j * CLT_NT;
         if (r < n) {
             const uint32_t c = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
                                __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(256) void k_count_lm_tiles(int64_t n, const unsigne
         }
     }
     uint32_t tot;
-    block_excl_scan<256>(s, lds, &tot);
+    block_excl_scan<CLT_NT>(s, lds, &tot);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
 }
 
@@ -584,7 +586,8 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
                                                   const uint64_t* __restrict__ ndesc, const uint64_t* __restrict__ plo,
                                                   const uint64_t* __restrict__ phi, uint64_t* __restrict__ olo,
                                                   uint64_t* __restrict__ ohi, uint32_t* __restrict__ opar,
-                                                  uint32_t* __restrict__ first, int desc_in_idx) {
+                                                  uint32_t* __restrict__ first, int desc_in_idx,
+                                                  unsigned long long* __restrict__ zlost) {
     __shared__ uint32_t f[256];
     __shared__ uint32_t card[NCARDS];
     __shared__ int32_t pdelta[4][NPAT_MAX];
@@ -613,9 +616,23 @@ __global__ __launch_bounds__(256) void k_gather_d(const Tables* __restrict__ T, 
         ohi[i] = chi;
         opar[i] = r;
         atomicMin(&f[st_pts(chi)], (uint32_t)i);
+        if (zlost) {   // the next turn's lost marks of parent i start at zero (no 24 B/parent memset before it)
+            zlost[i * 3] = 0ull;
+            zlost[i * 3 + 1] = 0ull;
+            zlost[i * 3 + 2] = 0ull;
+        }
     }
     __syncthreads();
     if (f[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&first[threadIdx.x], f[threadIdx.x]);
+}
+
+__global__ void k_front_reset(unsigned long long* __restrict__ nraw, uint32_t* __restrict__ small) {
+    const int t = threadIdx.x;
+    if (t == 0) {
+        *nraw = 0ull;
+        small[264] = 0u;
+    }
+    if (t < 6) small[2 + t] = 0u;
 }
 
 __global__ void k_pts_first(const uint64_t* __restrict__ bhi, int64_t m, uint32_t* __restrict__ first) {
@@ -969,7 +986,8 @@ static void preallocate_dist(Engine& E) {
     E.part_hist.ensure(dtiles * (size_t)std::max(1, (int)E.cfg.world_size) + 80 + 16 * 64);
     E.kidx.ensure(wl);
     E.rkey.ensure(wl);
-    topk_reserve(E.topk, (int64_t)wl, (int64_t)wl);   // the receive sort only (the joint select is k_ds_*)
+    topk_reserve(E.topk, (int64_t)wl, (int64_t)wl);   // the receive sort (the joint select is k_ds_*) ...
+    E.topk.tile_a.ensure(dtiles + 1);                 // ... and the joint select's tie / destination tiles
     E.scan.tiles.ensure(nr / SCAN_TILE + 1);
     E.turn_mem.reserve(wl * 20 * 24);
 }
@@ -1007,6 +1025,26 @@ static hipEvent_t* tev(Engine& E, int turn) {
 // previous gather): expansion + claims, survivor counts and offsets, then one readback of the
 // small state: n_unique, error word, the beam's per-pts first-rank table (gather) and n_raw.  The
 // next sb_step waits on this readback only — the goal check and the sizes come from one round trip.
+// The engine stream and the noise producers' side stream.  SB_STREAM_PRIO=1: the side stream at the lowest
+// priority, the engine stream at the highest, so a noise chunk's kernels would take only CUs the step's
+// kernels leave (a chunk's placement kernel landing on the emission cost it ~100 us in one traced turn).
+// A/B over three interleaved rounds (profiles/r3/s5/ab_front.txt): 866.7 M states/s either way (the
+// expansion's box drift, 3.19-3.52 ms, is larger than any effect); off by default
+#ifndef SB_STREAM_PRIO
+#define SB_STREAM_PRIO 0
+#endif
+static void create_streams(hipStream_t& s, hipStream_t& s_mt) {
+    int least = 0, greatest = 0;
+    if (SB_STREAM_PRIO) SB_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    if (SB_STREAM_PRIO && least != greatest) {
+        SB_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest));
+        SB_HIP(hipStreamCreateWithPriority(&s_mt, hipStreamNonBlocking, least));
+    } else {
+        SB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        SB_HIP(hipStreamCreateWithFlags(&s_mt, hipStreamNonBlocking));
+    }
+}
+
 static void launch_front(Engine& E) {
     const bool timing = E.cfg.flags & 1;
     Turn& cur = E.turns.back();
@@ -1020,14 +1058,13 @@ static void launch_front(Engine& E) {
     if (E.lost.p != lost_was) E.lost_zero = 0;   // reallocated
     E.cnt.ensure((size_t)n);
     E.off.ensure((size_t)n);
-    SB_HIP(hipMemsetAsync(E.d_nraw, 0, 8, E.s));
     {
         const int64_t z = std::min<int64_t>(E.lost_zero, n);
         if (n > z) SB_HIP(hipMemsetAsync(E.lost.p + (size_t)z * 3, 0, (size_t)(n - z) * 24, E.s));
         E.lost_zero = 0;   // the expansion below marks [0, n)
     }
-    SB_HIP(hipMemsetAsync(E.d_small + 2, 0, 6 * 4, E.s));   // claim statistics (SB_CLAIM_STATS builds): [2..8)
-    SB_HIP(hipMemsetAsync(E.d_small + 264, 0, 4, E.s));     // k_expand's group counter
+    // raw count, claim statistics (SB_CLAIM_STATS builds: [2..8)) and k_expand's group counter: one launch
+    hipLaunchKernelGGL(k_front_reset, dim3(1), dim3(64), 0, E.s, E.d_nraw, E.d_small);
     const uint64_t turn_tag = (uint64_t)(E.turn + 1) << 40;
     if (timing) SB_HIP(hipEventRecord(ev[0], E.s));
     if (n > 0) {
@@ -1041,7 +1078,7 @@ static void launch_front(Engine& E) {
     if (timing) SB_HIP(hipEventRecord(ev[1], E.s));
     if (n > 0) {   // survivors per parent + their tile sums, then the offsets (next_queue order)
         E.scan.tiles.ensure((size_t)((n + SCAN_TILE - 1) / SCAN_TILE));
-        hipLaunchKernelGGL(k_count_lm_tiles, dim3((unsigned)((n + SCAN_TILE - 1) / SCAN_TILE)), dim3(256), 0, E.s, n,
+        hipLaunchKernelGGL(k_count_lm_tiles, dim3((unsigned)((n + SCAN_TILE - 1) / SCAN_TILE)), dim3(CLT_NT), 0, E.s, n,
                            E.cand.p, E.lost.p, E.cnt.p, E.scan.tiles.p);
         scan_exclusive_u32_sums(E.cnt.p, E.off.p, n, E.d_small, E.scan, E.s);
     } else {
@@ -1243,10 +1280,16 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
 #ifndef SB_GATHER_GRID
 #define SB_GATHER_GRID 4096   // blocks of the descriptor gather (each thread walks m / (256 * grid) kept states)
 #endif
-    if (desc)   // emission wrote descriptors only: rebuild the kept states from their parents
+#ifndef SB_GATHER_ZERO_LOST
+#define SB_GATHER_ZERO_LOST 0   // 1: the gather clears the next turn's lost marks instead of a memset before the
+                                // expansion.  A/B (profiles/r3/s5/ab_front.txt): gather +12-16 us, memset -14 us
+#endif
+    if (desc) {   // emission wrote descriptors only: rebuild the kept states from their parents
+        unsigned long long* zl = SB_GATHER_ZERO_LOST && E.lost.cap >= (size_t)m * 3 ? E.lost.p : nullptr;
         hipLaunchKernelGGL(k_gather_d, dim3(grid_cap(m, 256, SB_GATHER_GRID)), dim3(256), 0, E.s, E.d_tables, idx, m, E.nlo.p,
-                           cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8, (int)desc_pay);
-    else
+                           cur.lo, cur.hi, nt.lo, nt.hi, nt.par, E.d_small + 8, (int)desc_pay, zl);
+        if (zl) E.lost_zero = m;
+    } else
         hipLaunchKernelGGL(k_gather, dim3(grid_cap(m, 256, 4096)), dim3(256), 0, E.s, idx, m, E.nlo.p, E.nhi.p, E.npar.p,
                            nt.lo, nt.hi, nt.par, E.d_small + 8);
     if (timing) SB_HIP(hipEventRecord(ev[6], E.s));
@@ -1397,8 +1440,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         if (cfg->flags & 32) E.rec_per_parent = 48;   // compact sharded record buffers (several ranks per GPU)
         E.dev = cfg->device;
         SB_HIP(hipSetDevice(E.dev));
-        SB_HIP(hipStreamCreateWithFlags(&E.s, hipStreamNonBlocking));
-        SB_HIP(hipStreamCreateWithFlags(&E.s_mt, hipStreamNonBlocking));
+        create_streams(E.s, E.s_mt);
         for (auto& e : E.ev) SB_HIP(hipEventCreate(&e));
         E.d_tables = upload_tables(E.s);
         int lg = cfg->visited_log2;
