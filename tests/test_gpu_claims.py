@@ -83,3 +83,39 @@ def test_answer_bits_roundtrip():
             assert (o[:off] == 7).all() and (o[off + n:] == 7).all(), n
     finally:
         b.close()
+
+
+def test_answer_bits_segments_one_launch():
+    """sbd_pack_bits_segs / sbd_unpack_bits_segs (every (source, part) answer segment in one launch) against
+    numpy: 200 segments (more than one launch's table), empty and odd lengths, unaligned offsets, and bytes
+    outside the segments left untouched."""
+    rng = np.random.default_rng(11)
+    b = _backend(12)
+    try:
+        lens = rng.integers(0, 3000, 200)
+        lens[::17] = 0
+        lens[5] = 1
+        lens[6] = 8
+        src_off = np.concatenate([[3], 3 + np.cumsum(lens + rng.integers(0, 5, 200))[:-1]]).astype(np.int64)
+        nbytes = (lens + 7) // 8
+        dst_off = np.concatenate([[1], 1 + np.cumsum(nbytes + 1)[:-1]]).astype(np.int64)
+        src = (rng.random(int(src_off[-1] + lens[-1] + 8)) < 0.5).astype(np.uint8) * rng.integers(1, 255, int(src_off[-1] + lens[-1] + 8)).astype(np.uint8)
+        ds = torch.from_numpy(src).to(b.device)
+        packed = torch.zeros(int(dst_off[-1] + nbytes[-1] + 4), dtype=torch.uint8, device=b.device)
+        segs = [(int(src_off[s]), int(lens[s]), int(dst_off[s])) for s in range(200)]
+        b.pack_bits_segs(ds, segs, packed)
+        out = torch.full_like(ds, 7)
+        b.unpack_bits_segs(packed, [(int(dst_off[s]), int(lens[s]), int(src_off[s])) for s in range(200)], out)
+        torch.cuda.synchronize()
+        p, o = packed.cpu().numpy(), out.cpu().numpy()
+        want_p = np.zeros_like(p)
+        want_o = np.full_like(src, 7)
+        for s in range(200):
+            a, n, d = int(src_off[s]), int(lens[s]), int(dst_off[s])
+            bits = np.packbits((src[a:a + n] != 0).astype(np.uint8), bitorder='little')
+            want_p[d:d + len(bits)] = bits
+            want_o[a:a + n] = (src[a:a + n] != 0).astype(np.uint8)
+        assert np.array_equal(p, want_p)
+        assert np.array_equal(o, want_o)
+    finally:
+        b.close()
