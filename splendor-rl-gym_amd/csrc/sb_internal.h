@@ -110,6 +110,7 @@ struct TopkScratch {
     DBuf<uint64_t> sk;              // select: staged first-partition keys (one TK_TILE region per tile)
     DBuf<uint32_t> si;              // select: staged first-partition payloads
     uint32_t fx_epoch = 0;
+    uint32_t os_epoch = 0;          // LSD sort look-back granule epochs (SB_OS_EPOCH)
     void release();
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.

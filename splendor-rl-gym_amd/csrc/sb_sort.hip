@@ -53,6 +53,9 @@ constexpr int64_t TK_WRITE_GRID = SB_TK_WRITE_GRID;           // candidate passe
 #define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
 #endif
 constexpr int OS_PREFIX_BITS = SB_SORT_PREFIX_BITS;
+#ifndef SB_OS_EPOCH
+#define SB_OS_EPOCH 1            // look-back granules stamped with a per-call epoch (no clearing memset per call)
+#endif
 #ifndef SB_TK_STAGE
 #define SB_TK_STAGE 1            // first partition: one read, staged per tile (0: count + write, two reads)
 #endif
@@ -643,7 +646,7 @@ __global__ void k_iota(uint32_t* v, const uint64_t* keys, uint64_t* okeys, int64
 // bits that vary among the kept keys: [lowest kept, max]; lowest kept >= prefix << sh
 // The kept keys lie in [lo, max]: sorting key - lo (same order) needs only the bits of max - lo,
 // one digit fewer than the bits in which lo and max differ when the range crosses a power of two.
-__global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) {
+__device__ __forceinline__ void tk_sortsetup_body(uint64_t* st, int selected, int prefix_bits) {
     uint64_t lo = st[ST_MIN];
     if (selected) lo = st[ST_SH] >= 64 ? 0ull : (st[ST_PREFIX] << st[ST_SH]);
     const uint64_t x = st[ST_MAX] - lo;
@@ -654,6 +657,7 @@ __global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) {
     st[ST_FXN] = 0;
     st[ST_FXI] = 0;
 }
+__global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) { tk_sortsetup_body(st, selected, prefix_bits); }
 
 // ---- stable LSD radix sort of the kept set, one kernel per 8-bit digit (decoupled look-back)
 // Digit p of key k is (~(k - SLO) >> 8p) & 255 (ascending digits = descending keys).  k_os_hist builds the
@@ -691,6 +695,12 @@ constexpr int OS_ERR = OS_TICKET + 4;             // spin-limit flag
 constexpr int OS_HDR = OS_ERR + 4;                // 16-B aligned
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+// sort setup + the look-back buffer's header (digit histograms, tickets, error word) cleared: one launch
+__global__ void k_os_begin(uint64_t* st, int selected, int prefix_bits, uint64_t* __restrict__ lb) {
+    if (threadIdx.x == 0) tk_sortsetup_body(st, selected, prefix_bits);
+    for (int i = threadIdx.x; i < OS_HDR; i += blockDim.x) lb[i] = 0;
+}
 
 __device__ __forceinline__ void os_publish(uint64_t* p, uint64_t v) {
     __hip_atomic_store((gu64_t*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -784,8 +794,11 @@ __global__ __launch_bounds__(256) void k_os_hsum(const uint32_t* __restrict__ pa
 // the tile's global offsets per digit: exclusive scan over the earlier tiles' published counts (look
 // back over the predecessors, OS_LB granules polled together: add counts until the first inclusive one;
 // wait where a predecessor has not published yet) plus the global start of the digit
-__device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int p, uint32_t agg, int t) {
-    const uint64_t ep = (uint64_t)(p + 1) << 34;
+// The granules' epoch (bits 34..63) is ebase + pass + 1: ebase advances by 8 every sort call, so granules left
+// by earlier calls never match and the look-back buffer needs no clearing per call (SB_OS_EPOCH)
+__device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int p, uint32_t agg, int t, uint32_t ebase) {
+    const uint64_t epv = (uint64_t)ebase + (uint64_t)(p + 1);
+    const uint64_t ep = epv << 34;
     uint64_t* mine = lb + OS_HDR + tile * 256 + t;
     uint32_t excl = 0;
     if (tile == 0 || (SB_OS_DBG & 1)) {   // DBG 1 (timing only): no look-back
@@ -802,7 +815,7 @@ __device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int 
         int u = 0;
         bool done = false;
         for (; u < OS_LB; u++) {
-            if ((v[u] >> 34) != (uint64_t)(p + 1)) break;
+            if ((v[u] >> 34) != epv) break;
             excl += (uint32_t)v[u];
             if (v[u] & OS_INC) {
                 done = true;
@@ -826,7 +839,8 @@ __device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int 
 // atomic that returns the count before) and the group shares it — the element's rank among the wave's
 // equal digits in index order.  A digit's offset in the tile is the sum of the earlier waves' counts.
 __global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
-                                                   int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
+                                                   int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
+                                                   uint32_t ebase) {
     if (p >= sort_passes(st)) return;
     const uint64_t* kin = (p & 1) ? k1 : k0;
     const uint32_t* vin = (p & 1) ? v1 : v0;
@@ -886,7 +900,7 @@ __global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, 
                 wcnt[x][t] = agg;
                 agg += c;
             }
-            excl = os_lookback(lb, tile, p, agg, t);
+            excl = os_lookback(lb, tile, p, agg, t, ebase);
         }
         uint32_t tot;
         const uint32_t gstart = block_excl_scan<OS_PNT>(t < 256 ? gh[t] : 0u, lds, &tot);
@@ -1236,11 +1250,22 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #ifdef SB_DBG_EMPTY   // diagnostic: extra empty launches (kernel boundary cost)
     for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
 #endif
-    hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
     const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
     const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
+    const size_t lb_cap = s.os.cap;
     s.os.ensure(lb_words);
-    SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
+    uint32_t ebase = 0;
+    if (SB_OS_EPOCH) {   // granules of earlier calls carry older epochs: cleared only when (re)allocated or wrapped
+        if (s.os.cap != lb_cap || s.os_epoch >= (1u << 26)) {
+            SB_HIP(hipMemsetAsync(s.os.p, 0, s.os.cap * 8, st));
+            s.os_epoch = 0;
+        }
+        ebase = ++s.os_epoch * 8;
+        hipLaunchKernelGGL(k_os_begin, dim3(1), dim3(256), 0, st, stv, (int)selected, prefix_bits, s.os.p);
+    } else {
+        hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
+        SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
+    }
     const unsigned ohg = grid_for(m, OSH_NT * OS_IPT, SB_OSH_GRID);
     if (SB_OSH_2STAGE) s.osh_part.ensure((size_t)ohg * OSH_ROW);
     hipLaunchKernelGGL(k_os_hist, dim3(ohg), dim3(OSH_NT), 0, st, s.k0.p, m, stv, s.os.p, s.osh_part.p,
@@ -1254,7 +1279,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
     for (int p = 0; p < (prefix_bits + 7) / 8; p++)   // passes beyond the varying bits exit at once
         hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
-                           stv, s.os.p);
+                           stv, s.os.p, ebase);
     // exact order among keys that share their 32-bit prefix
     if (s.fx_mark.cap < (size_t)m) {   // run claims carry this call's epoch: zeroed only when (re)allocated
         s.fx_mark.ensure((size_t)m);
