@@ -659,8 +659,8 @@ __device__ __forceinline__ void tk_sortsetup_body(uint64_t* st, int selected, in
 }
 __global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) { tk_sortsetup_body(st, selected, prefix_bits); }
 
-// ---- stable LSD radix sort of the kept set, one kernel per 8-bit digit (decoupled look-back)
-// Digit p of key k is (~(k - SLO) >> 8p) & 255 (ascending digits = descending keys).  k_os_hist builds the
+// ---- stable LSD radix sort of the kept set, one kernel per OS_D-bit digit (decoupled look-back)
+// Digit p of key k is (~(k - SLO) >> OS_D p) & (OS_B - 1) (ascending digits = descending keys).  k_os_hist builds the
 // global histograms of every needed digit in one read.  Pass p: tiles of OS_TILE elements take
 // tickets in launch order; a tile ranks its elements stably ((round, wave) counts per digit + the
 // lane rank from a wave match), publishes its per-digit counts, looks back over its predecessors'
@@ -686,10 +686,20 @@ constexpr int OS_LB = SB_OS_LB;
 #ifndef SB_OS_DBG
 #define SB_OS_DBG 0      // timing diagnostics only (wrong order): 1 no look-back, 2 unscattered writes
 #endif
+#ifndef SB_OS_D
+#define SB_OS_D 8        // digit bits per LSD pass.  10 (four passes for the 40-bit prefix instead of five) measured
+                         // 132 us per pass against 51 (1024-digit look-back per tile, 229 VGPRs: 2 waves per SIMD):
+                         // the sort 257 -> 527 us per step (profiles/r3/s5/ab_sort_digits.txt)
+#endif
+constexpr int OS_D = SB_OS_D;
+constexpr int OS_B = 1 << OS_D;                     // bins per digit
+constexpr int OS_MAXP = (64 + OS_D - 1) / OS_D;     // passes over a full 64-bit key
+constexpr int OS_DPT = OS_B / OS_PNT;               // digits owned per pass thread (consecutive)
+static_assert(OS_B % OS_PNT == 0 && OS_MAXP <= 8, "digit width vs pass workgroup");
 constexpr uint64_t OS_AGG = 1ull << 32, OS_INC = 2ull << 32;
 constexpr uint32_t OS_SPIN_MAX = 1u << 26;
-// control words at the start of the look-back buffer (u64): [0, 2048) histograms (u32 pairs), tickets
-constexpr int OS_HIST_WORDS = 8 * 256 / 2;
+// control words at the start of the look-back buffer (u64): the digit histograms (u32 pairs), tickets
+constexpr int OS_HIST_WORDS = OS_MAXP * OS_B / 2;
 constexpr int OS_TICKET = OS_HIST_WORDS;          // 8 u32 tickets in 4 words
 constexpr int OS_ERR = OS_TICKET + 4;             // spin-limit flag
 constexpr int OS_HDR = OS_ERR + 4;                // 16-B aligned
@@ -709,7 +719,7 @@ __device__ __forceinline__ uint64_t os_poll(const uint64_t* p) {
     return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] - st[ST_SH32] + 7) / 8); }
+__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] - st[ST_SH32] + OS_D - 1) / OS_D); }
 __device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64_t sh) { return (k - slo) >> sh; }
 
 // histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
@@ -725,25 +735,26 @@ constexpr int OSH_NT = SB_OSH_NT;
 #ifndef SB_OSH_WH
 #define SB_OSH_WH 1          // per-wave sub-histograms (less LDS atomic contention between waves)
 #endif
-constexpr int OSH_NH = SB_OSH_WH ? (OSH_NT / 64 < 8 ? OSH_NT / 64 : 8) : 1;   // at most 8 (64 KB of LDS)
+constexpr int OSH_NHMAX = 65536 / (OS_MAXP * OS_B * 4) < 1 ? 1 : 65536 / (OS_MAXP * OS_B * 4);   // 64 KB of LDS
+constexpr int OSH_NH = SB_OSH_WH ? (OSH_NT / 64 < OSH_NHMAX ? OSH_NT / 64 : OSH_NHMAX) : 1;
 // Flush of the blocks' histograms: one atomic per (block, bin).  The two-stage flush (SB_OSH_2STAGE:
 // each block stores its row of P*256 counts, k_os_hsum adds 32 rows per thread with one atomic per
 // (column, 32 rows)) was measured no faster: the same-address atomics are not what bounds k_os_hist.
 #ifndef SB_OSH_2STAGE
 #define SB_OSH_2STAGE 0   // A/B: no faster (profiles/r2_ab_hist_flush.txt)
 #endif
-constexpr int OSH_ROW = 8 * 256;     // u32 per block row (digits 0..7)
+constexpr int OSH_ROW = OS_MAXP * OS_B;   // u32 per block row (every digit)
 constexpr int OSH_RCHUNK = 32;       // rows per k_os_hsum thread
 // first_dev (optional): count only keys[*first_dev ..) (the rest were counted where they were written)
 __global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__ keys, int64_t n,
                                                     const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
                                                     uint32_t* __restrict__ part, const uint64_t* __restrict__ first_dev) {
-    __shared__ uint32_t hh[OSH_NH][8][256];
+    __shared__ uint32_t hh[OSH_NH][OS_MAXP][OS_B];
     const int P = sort_passes(st);
     const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
-    for (int i = threadIdx.x; i < OSH_NH * 8 * 256; i += OSH_NT) (&hh[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < OSH_NH * OS_MAXP * OS_B; i += OSH_NT) (&hh[0][0][0])[i] = 0;
     __syncthreads();
-    uint32_t (*h)[256] = hh[SB_OSH_WH ? ((threadIdx.x >> 6) % OSH_NH) : 0];
+    uint32_t (*h)[OS_B] = hh[SB_OSH_WH ? ((threadIdx.x >> 6) % OSH_NH) : 0];
     const uint64_t lt = lanemask_lt();
     const int64_t stride = (int64_t)gridDim.x * OSH_NT;
     const int64_t i_lo = first_dev ? (int64_t)*first_dev : 0;
@@ -756,7 +767,7 @@ __global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__
             const bool valid = i0 + r * stride < n;
             if (!__ballot(valid)) break;
             for (int p = 0; p < P; p++) {
-                const int b = valid ? (int)((kk[r] >> (8 * p)) & 255) : -1;
+                const int b = valid ? (int)((kk[r] >> (OS_D * p)) & (OS_B - 1)) : -1;
                 const uint64_t act = __ballot(b >= 0);
                 const int b0 = __shfl(b, __builtin_ctzll(act), 64);
                 const uint64_t same = __ballot(b == b0);
@@ -770,7 +781,7 @@ __global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__
     }
     __syncthreads();
     uint32_t* gh = reinterpret_cast<uint32_t*>(lb);
-    for (int i = threadIdx.x; i < P * 256; i += OSH_NT) {
+    for (int i = threadIdx.x; i < P * OS_B; i += OSH_NT) {
         uint32_t c = 0;
 #pragma unroll
         for (int v = 0; v < OSH_NH; v++) c += (&hh[v][0][0])[i];
@@ -782,7 +793,7 @@ __global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__
 __global__ __launch_bounds__(256) void k_os_hsum(const uint32_t* __restrict__ part, int rows,
                                                  const uint64_t* __restrict__ st, uint64_t* __restrict__ lb) {
     const int col = blockIdx.x * 256 + threadIdx.x;
-    if (col >= sort_passes(st) * 256) return;
+    if (col >= sort_passes(st) * OS_B) return;
     const int r0 = blockIdx.y * OSH_RCHUNK;
     uint32_t c = 0;
 #pragma unroll
@@ -796,41 +807,64 @@ __global__ __launch_bounds__(256) void k_os_hsum(const uint32_t* __restrict__ pa
 // wait where a predecessor has not published yet) plus the global start of the digit
 // The granules' epoch (bits 34..63) is ebase + pass + 1: ebase advances by 8 every sort call, so granules left
 // by earlier calls never match and the look-back buffer needs no clearing per call (SB_OS_EPOCH)
-__device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int p, uint32_t agg, int t, uint32_t ebase) {
+// The thread owns OS_DPT consecutive digits d0 ..: their look-backs run together (every poll of a round issued
+// before any is used).
+__device__ __forceinline__ void os_lookback(uint64_t* lb, int64_t tile, int p, const uint32_t* agg, int d0,
+                                            uint32_t ebase, uint32_t* excl) {
     const uint64_t epv = (uint64_t)ebase + (uint64_t)(p + 1);
     const uint64_t ep = epv << 34;
-    uint64_t* mine = lb + OS_HDR + tile * 256 + t;
-    uint32_t excl = 0;
-    if (tile == 0 || (SB_OS_DBG & 1)) {   // DBG 1 (timing only): no look-back
-        os_publish(mine, ep | OS_INC | agg);
-        return 0;
-    }
-    os_publish(mine, ep | OS_AGG | agg);
-    int64_t j = tile - 1;
-    uint32_t spins = 0;
-    for (;;) {
-        uint64_t v[OS_LB];
+    uint64_t* mine = lb + OS_HDR + tile * OS_B + d0;
 #pragma unroll
-        for (int u = 0; u < OS_LB; u++) v[u] = j - u >= 0 ? os_poll(lb + OS_HDR + (j - u) * 256 + t) : (ep | OS_INC);
-        int u = 0;
-        bool done = false;
-        for (; u < OS_LB; u++) {
-            if ((v[u] >> 34) != epv) break;
-            excl += (uint32_t)v[u];
-            if (v[u] & OS_INC) {
-                done = true;
-                break;
+    for (int k = 0; k < OS_DPT; k++) excl[k] = 0;
+    if (tile == 0 || (SB_OS_DBG & 1)) {   // DBG 1 (timing only): no look-back
+#pragma unroll
+        for (int k = 0; k < OS_DPT; k++) os_publish(mine + k, ep | OS_INC | agg[k]);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < OS_DPT; k++) os_publish(mine + k, ep | OS_AGG | agg[k]);
+    int64_t j[OS_DPT];
+    bool done[OS_DPT];
+#pragma unroll
+    for (int k = 0; k < OS_DPT; k++) {
+        j[k] = tile - 1;
+        done[k] = false;
+    }
+    int left = OS_DPT;
+    uint32_t spins = 0;
+    while (left > 0) {
+        uint64_t v[OS_DPT][OS_LB];
+#pragma unroll
+        for (int k = 0; k < OS_DPT; k++)
+#pragma unroll
+            for (int u = 0; u < OS_LB; u++)
+                v[k][u] = !done[k] && j[k] - u >= 0 ? os_poll(lb + OS_HDR + (j[k] - u) * OS_B + d0 + k) : (ep | OS_INC);
+        bool stalled = false;
+#pragma unroll
+        for (int k = 0; k < OS_DPT; k++) {
+            if (done[k]) continue;
+            int u = 0;
+            for (; u < OS_LB; u++) {
+                if ((v[k][u] >> 34) != epv) break;
+                excl[k] += (uint32_t)v[k][u];
+                if (v[k][u] & OS_INC) {
+                    done[k] = true;
+                    left--;
+                    break;
+                }
+            }
+            if (!done[k]) {
+                j[k] -= u;
+                stalled |= u < OS_LB;
             }
         }
-        if (done) break;
-        j -= u;
-        if (u < OS_LB && ++spins > OS_SPIN_MAX) {   // bounded: a lost predecessor shows up as an error, not a hang
+        if (stalled && ++spins > OS_SPIN_MAX) {   // bounded: a lost predecessor shows up as an error, not a hang
             atomicOr(reinterpret_cast<uint32_t*>(lb + OS_ERR), 1u);
             break;
         }
     }
-    os_publish(mine, ep | OS_INC | (uint64_t)(excl + agg));
-    return excl;
+#pragma unroll
+    for (int k = 0; k < OS_DPT; k++) os_publish(mine + k, ep | OS_INC | (uint64_t)(excl[k] + agg[k]));
 }
 
 // Wave-sequential ranking: wave w owns the contiguous sub-tile [w * 64 * OS_IPT, (w + 1) * 64 * OS_IPT) of
@@ -838,7 +872,11 @@ __device__ __forceinline__ uint32_t os_lookback(uint64_t* lb, int64_t tile, int 
 // equal digits, the group leader adds the group size to the wave's running count of that digit (an LDS
 // atomic that returns the count before) and the group shares it — the element's rank among the wave's
 // equal digits in index order.  A digit's offset in the tile is the sum of the earlier waves' counts.
-__global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
+#ifndef SB_OS_WAVES
+#define SB_OS_WAVES 0   // 0: the compiler's register choice (155 VGPRs: 3 waves per SIMD).  4 (128 VGPRs, a 104 B
+                        // spill) measured slower: 257 -> 341 us per step (profiles/r3/s5/ab_sort_digits.txt)
+#endif
+__global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
                                                    int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
                                                    uint32_t ebase) {
     if (p >= sort_passes(st)) return;
@@ -846,27 +884,27 @@ __global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, 
     const uint32_t* vin = (p & 1) ? v1 : v0;
     uint64_t* kout = (p & 1) ? k0 : k1;
     uint32_t* vout = (p & 1) ? v0 : v1;
-    __shared__ uint32_t wcnt[OS_NW][256];   // running digit counts per wave, then exclusive offsets in the tile
-    __shared__ uint32_t sbase[256];
+    __shared__ uint32_t wcnt[OS_NW][OS_B];   // running digit counts per wave, then exclusive offsets in the tile
+    __shared__ uint32_t sbase[OS_B];
     __shared__ uint32_t lds[OS_NW + 1];
     __shared__ uint32_t s_tile;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(lb + OS_TICKET);
     const int64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
-    const int shift = 8 * p;
+    const int shift = OS_D * p;
     const uint64_t slo = st[ST_SLO], psh = st[ST_SH32];
     const uint64_t lt = lanemask_lt();
-    const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * 256;
+    const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * OS_B;
     for (int it = 0;; it++) {
         if (t == 0) s_tile = (SB_OS_DBG & 4) ? (it ? 0xFFFFFFFFu : blockIdx.x) : atomicAdd(&ticket[p], 1u);   // DBG 4: block order
-        for (int i = t; i < OS_NW * 256; i += OS_PNT) (&wcnt[0][0])[i] = 0;
+        for (int i = t; i < OS_NW * OS_B; i += OS_PNT) (&wcnt[0][0])[i] = 0;
         __syncthreads();
         const int64_t tile = s_tile;
         if (tile >= ntiles) return;
         const int64_t base = tile * OS_TILE + (int64_t)w * (64 * OS_IPT) + l;
         uint64_t kk[OS_IPT];
         uint32_t vv[OS_IPT];
-        uint32_t rk[OS_IPT];   // digit | rank among the wave's equal digits << 8
+        uint32_t rk[OS_IPT];   // digit | rank among the wave's equal digits << OS_D
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const int64_t i = base + (int64_t)r * 64;
@@ -876,10 +914,10 @@ __global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, 
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const bool valid = base + (int64_t)r * 64 < n;
-            const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & 255);
+            const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & (OS_B - 1));
             uint64_t peers = __ballot(valid);
 #pragma unroll
-            for (int b = 0; b < 8; b++) {
+            for (int b = 0; b < OS_D; b++) {
                 const uint64_t bb = __ballot((d >> b) & 1);
                 peers &= ((d >> b) & 1) ? bb : ~bb;
             }
@@ -887,31 +925,40 @@ __global__ __launch_bounds__(OS_PNT) void k_os_pass(uint64_t* k0, uint32_t* v0, 
             uint32_t before = 0;
             if (valid && leader == l) before = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
             before = __shfl(before, leader, 64);
-            rk[r] = d | ((before + (uint32_t)__popcll(peers & lt)) << 8);
+            rk[r] = d | ((before + (uint32_t)__popcll(peers & lt)) << OS_D);
         }
         __syncthreads();
-        // thread t < 256 owns digit t: the waves' exclusive offsets and the tile aggregate
-        uint32_t excl = 0;
-        if (t < 256) {
-            uint32_t agg = 0;
+        // thread t owns digits t * OS_DPT ..: the waves' exclusive offsets and the tile aggregates
+        const int d0 = t * OS_DPT;
+        uint32_t agg[OS_DPT], excl[OS_DPT], gv[OS_DPT], gsum = 0;
+#pragma unroll
+        for (int k = 0; k < OS_DPT; k++) {
+            uint32_t a = 0;
 #pragma unroll
             for (int x = 0; x < OS_NW; x++) {
-                const uint32_t c = wcnt[x][t];
-                wcnt[x][t] = agg;
-                agg += c;
+                const uint32_t c = wcnt[x][d0 + k];
+                wcnt[x][d0 + k] = a;
+                a += c;
             }
-            excl = os_lookback(lb, tile, p, agg, t, ebase);
+            agg[k] = a;
+            gv[k] = gh[d0 + k];
+            gsum += gv[k];
         }
+        os_lookback(lb, tile, p, agg, d0, ebase, excl);
         uint32_t tot;
-        const uint32_t gstart = block_excl_scan<OS_PNT>(t < 256 ? gh[t] : 0u, lds, &tot);
-        if (t < 256) sbase[t] = gstart + excl;
+        uint32_t run = block_excl_scan<OS_PNT>(gsum, lds, &tot);   // global start of each digit
+#pragma unroll
+        for (int k = 0; k < OS_DPT; k++) {
+            sbase[d0 + k] = run + excl[k];
+            run += gv[k];
+        }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const int64_t i = base + (int64_t)r * 64;
             if (i < n) {
-                const uint32_t d = rk[r] & 255;
-                const uint32_t o = (SB_OS_DBG & 2) ? (uint32_t)i : sbase[d] + wcnt[w][d] + (rk[r] >> 8);
+                const uint32_t d = rk[r] & (OS_B - 1);
+                const uint32_t o = (SB_OS_DBG & 2) ? (uint32_t)i : sbase[d] + wcnt[w][d] + (rk[r] >> OS_D);
                 kout[o] = kk[r];
                 vout[o] = vv[r];
             }
@@ -1154,7 +1201,7 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
         s.sk.ensure((size_t)(n / TK_TILE + 1) * TK_TILE);
         s.si.ensure((size_t)(n / TK_TILE + 1) * TK_TILE);
     }
-    s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * 256);
+    s.os.ensure((size_t)OS_HDR + (size_t)(m / OS_TILE + 1) * OS_B);
     s.small.ensure(ST_WORDS);
     s.fx_list.ensure((size_t)m);
     if (SB_OSH_2STAGE) s.osh_part.ensure((size_t)grid_for(m, OS_NT * OS_IPT, SB_OSH_GRID) * OSH_ROW);
@@ -1251,7 +1298,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
 #endif
     const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
-    const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * 256;
+    const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * OS_B;
     const size_t lb_cap = s.os.cap;
     s.os.ensure(lb_words);
     uint32_t ebase = 0;
@@ -1271,13 +1318,13 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     hipLaunchKernelGGL(k_os_hist, dim3(ohg), dim3(OSH_NT), 0, st, s.k0.p, m, stv, s.os.p, s.osh_part.p,
                        (const uint64_t*)nullptr);
     if (SB_OSH_2STAGE)
-        hipLaunchKernelGGL(k_os_hsum, dim3(8, (ohg + OSH_RCHUNK - 1) / OSH_RCHUNK), dim3(256), 0, st, s.osh_part.p,
+        hipLaunchKernelGGL(k_os_hsum, dim3(OS_MAXP * OS_B / 256, (ohg + OSH_RCHUNK - 1) / OSH_RCHUNK), dim3(256), 0, st, s.osh_part.p,
                            (int)ohg, stv, s.os.p);
 #ifndef SB_OS_GRID
 #define SB_OS_GRID 1u << 20   // blocks per pass at most (tiles beyond are taken by ticket)
 #endif
     const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
-    for (int p = 0; p < (prefix_bits + 7) / 8; p++)   // passes beyond the varying bits exit at once
+    for (int p = 0; p < (prefix_bits + OS_D - 1) / OS_D; p++)   // passes beyond the varying bits exit at once
         hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
                            stv, s.os.p, ebase);
     // exact order among keys that share their 32-bit prefix
