@@ -527,15 +527,10 @@ __global__ __launch_bounds__(XP_NT, SB_XP_WAVES) void k_expand(const Tables* __r
 }
 
 // ------------------------------------------------------------------ survivors of the lost-marking path
-__global__ __launch_bounds__(256) void k_count_lm(int64_t n, const unsigned long long* __restrict__ cand,
-                                                  const unsigned long long* __restrict__ lost, uint32_t* __restrict__ cnt) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-        cnt[r] = __popcll(cand[r * 3] & ~lost[r * 3]) + __popcll(cand[r * 3 + 1] & ~lost[r * 3 + 1]) +
-                 __popcll(cand[r * 3 + 2] & ~lost[r * 3 + 2]);
-}
-// the same with the scan's first kernel folded in: a block counts one SCAN_TILE tile of parents (strided,
-// coalesced) and stores the tile's sum for scan_exclusive_u32_sums (k_scan_reduce would read cnt again).
-// (1024 threads with every mask load issued first measured slower: 52-60 against 43-47 us)
+// survivors per parent = popcount(cand & ~lost) over the move space, with the scan's first kernel folded in:
+// a block counts one SCAN_TILE tile of parents (strided, coalesced) and stores the tile's sum for
+// scan_exclusive_u32_sums (k_scan_reduce would read cnt again).  (1024 threads with every mask load issued
+// first measured slower: 52-60 against 43-47 us)
 constexpr int CLT_NT = 256;
 __global__ __launch_bounds__(CLT_NT) void k_count_lm_tiles(int64_t n, const unsigned long long* __restrict__ cand,
                                                            const unsigned long long* __restrict__ lost,
