@@ -399,9 +399,13 @@ __global__ __launch_bounds__(TK_NT) void k_tk_count(const uint64_t* __restrict__
 // phase 2 also sets the output bases of groups 2 and 3.  Thread t scans SC_PER consecutive tiles in
 // registers; one workgroup scan per SC_PER * 1024 tiles.
 constexpr int SC_PER = 16;
+__device__ __forceinline__ void tk_sortsetup_body(uint64_t* st, int selected, int prefix_bits);
+// lb (the final partition's scan, SB_OS_EPOCH): the select's state is final here, so this one workgroup also
+// does the sort's setup and clears the look-back buffer's hdr_words header words (no k_os_begin launch)
 __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uint32_t* __restrict__ eq, int64_t n_host,
                                                    const uint64_t* __restrict__ n_dev, uint64_t* st, int slot_gt,
-                                                   int slot_eq, int phase2) {
+                                                   int slot_eq, int phase2, uint64_t* __restrict__ lb = nullptr,
+                                                   int hdr_words = 0, int prefix_bits = 0) {
     __shared__ uint32_t lds[1024 / 64 + 1];
     const int64_t ntiles = ((n_dev ? (int64_t)*n_dev : n_host) + TK_TILE - 1) / TK_TILE;
     uint32_t cg = 0, ce = 0;
@@ -436,6 +440,10 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
             st[ST_BASE2] = st[ST_A];
             st[ST_BASE3] = st[ST_A] + cg;
         }
+    }
+    if (lb) {
+        if (threadIdx.x == 0) tk_sortsetup_body(st, 1, prefix_bits);
+        for (int i = threadIdx.x; i < hdr_words; i += blockDim.x) lb[i] = 0;
     }
 }
 
@@ -978,10 +986,20 @@ constexpr int FX_NT = 256;
 constexpr int FX_SET = 1024;   // distinct keys per run (more sets error bit 32: never expected)
 constexpr int FX_LIST = 256;   // distinct keys placed by the compact start computation
 
+// out (SB_FX_COPY): the sorted payloads are copied to out here (k_fx_fix rewrites the runs it re-places), and
+// the look-back's spin-limit flag is reported — k_copy_idx's work without its launch
 __global__ __launch_bounds__(256) void k_fx_mark(const uint64_t* k0, const uint64_t* k1, int64_t m, uint64_t* st,
-                                                 uint32_t* __restrict__ list) {
-    const uint64_t* kf = (sort_passes(st) & 1) ? k1 : k0;
+                                                 uint32_t* __restrict__ list, const uint32_t* v0, const uint32_t* v1,
+                                                 uint32_t* __restrict__ out, const uint64_t* lb, uint32_t* err) {
+    const int P = sort_passes(st);
+    const uint64_t* kf = (P & 1) ? k1 : k0;
     const uint64_t slo = st[ST_SLO], sh = st[ST_SH32];
+    if (out) {
+        if (err && blockIdx.x == 0 && threadIdx.x == 0 && lb[OS_ERR]) atomicOr(err, 4u);
+        const uint32_t* vf = (P & 1) ? v1 : v0;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+            out[i] = vf[i];
+    }
     if (sh == 0) return;   // the prefix is the whole key: nothing to fix
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t a = kf[i - 1], b = kf[i];
@@ -992,7 +1010,7 @@ __global__ __launch_bounds__(256) void k_fx_mark(const uint64_t* k0, const uint6
     }
 }
 
-__global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t m,
+__global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint32_t* out, int64_t m,
                                                   uint64_t* st, const uint32_t* __restrict__ list,
                                                   uint32_t* __restrict__ runmark, uint32_t epoch, uint32_t* err) {
     const int P = sort_passes(st);
@@ -1133,6 +1151,7 @@ __global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, ui
         for (int64_t q = a + t; q < b; q += FX_NT) {
             kf[q] = ka[q];
             vf[q] = va[q];
+            if (out) out[q] = va[q];
         }
         __syncthreads();
     }
@@ -1235,6 +1254,21 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     s.small.ensure(ST_WORDS);
     uint64_t* stv = s.small.p;
     const bool selected = n > keep;
+    // the sort's look-back buffer: granules of earlier calls carry older epochs (SB_OS_EPOCH), so it is cleared
+    // only when (re)allocated or when the epochs wrap; its header is cleared with the sort's setup below
+    const int64_t ntiles_s = (m + OS_TILE - 1) / OS_TILE;
+    const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles_s * OS_B;
+    const size_t lb_cap = s.os.cap;
+    s.os.ensure(lb_words);
+    uint32_t ebase = 0;
+    if (SB_OS_EPOCH) {
+        if (s.os.cap != lb_cap || s.os_epoch >= (1u << 26)) {
+            SB_HIP(hipMemsetAsync(s.os.p, 0, s.os.cap * 8, st));
+            s.os_epoch = 0;
+        }
+        ebase = ++s.os_epoch * 8;
+    }
+    bool sort_begun = false;   // the setup + header clear rode on the final partition's scan
     if (fused && selected) {
         hipLaunchKernelGGL(k_tk_begin_fused, dim3(1), dim3(TK_NT), 0, st, stv, (int64_t)m, n);
     } else {
@@ -1287,7 +1321,8 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         // candidates above T -> group 2, the first NEED ties -> group 3
         hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
         hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, nc, stv, (int)ST_G2,
-                           (int)ST_E2, 1);
+                           (int)ST_E2, 1, SB_OS_EPOCH ? s.os.p : (uint64_t*)nullptr, (int)OS_HDR, prefix_bits);
+        sort_begun = SB_OS_EPOCH;
         hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
                            s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
                            stv + ST_NEED, (const uint32_t*)nullptr);
@@ -1297,18 +1332,9 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #ifdef SB_DBG_EMPTY   // diagnostic: extra empty launches (kernel boundary cost)
     for (int e = 0; e < SB_DBG_EMPTY; e++) hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
 #endif
-    const int64_t ntiles = (m + OS_TILE - 1) / OS_TILE;
-    const size_t lb_words = (size_t)OS_HDR + (size_t)ntiles * OS_B;
-    const size_t lb_cap = s.os.cap;
-    s.os.ensure(lb_words);
-    uint32_t ebase = 0;
-    if (SB_OS_EPOCH) {   // granules of earlier calls carry older epochs: cleared only when (re)allocated or wrapped
-        if (s.os.cap != lb_cap || s.os_epoch >= (1u << 26)) {
-            SB_HIP(hipMemsetAsync(s.os.p, 0, s.os.cap * 8, st));
-            s.os_epoch = 0;
-        }
-        ebase = ++s.os_epoch * 8;
-        hipLaunchKernelGGL(k_os_begin, dim3(1), dim3(256), 0, st, stv, (int)selected, prefix_bits, s.os.p);
+    const int64_t ntiles = ntiles_s;
+    if (SB_OS_EPOCH) {
+        if (!sort_begun) hipLaunchKernelGGL(k_os_begin, dim3(1), dim3(256), 0, st, stv, (int)selected, prefix_bits, s.os.p);
     } else {
         hipLaunchKernelGGL(k_tk_sortsetup, dim3(1), dim3(1), 0, st, stv, (int)selected, prefix_bits);
         SB_HIP(hipMemsetAsync(s.os.p, 0, lb_words * 8, st));
@@ -1335,13 +1361,19 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     }
     const uint32_t epoch = ++s.fx_epoch;
     s.fx_list.ensure((size_t)m);
-    hipLaunchKernelGGL(k_fx_mark, dim3(grid_for(m, 256, 2048)), dim3(256), 0, st, s.k0.p, s.k1.p, m, stv, s.fx_list.p);
+#ifndef SB_FX_COPY
+#define SB_FX_COPY 1   // the payload copy to out_idx in k_fx_mark / k_fx_fix instead of a k_copy_idx launch
+#endif
+    uint32_t* fxo = SB_FX_COPY ? out_idx : nullptr;
+    hipLaunchKernelGGL(k_fx_mark, dim3(grid_for(m, 256, 2048)), dim3(256), 0, st, s.k0.p, s.k1.p, m, stv, s.fx_list.p,
+                       s.v0.p, s.v1.p, fxo, s.os.p, err);
 #ifndef SB_FX_GRID
 #define SB_FX_GRID 64   // fix-up workgroups (each takes flagged positions until none are left)
 #endif
-    hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, stv, s.fx_list.p,
+    hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, fxo, m, stv, s.fx_list.p,
                        s.fx_mark.p, epoch, err);
-    hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
+    if (!fxo)
+        hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
     return m;
 }
