@@ -831,6 +831,7 @@ struct Engine {
     int front_turn = -1;                    // turn whose front half (expand .. readback) is in flight
     bool lookahead = true;                  // finish_turn launches the next front half (sb_set_lookahead)
     int64_t lost_zero = 0;                  // lost[0 .. 3 * lost_zero) is known zero (the emission cleared it)
+    bool first_reset = false;               // this turn's first-rank table was reset with the top-k's range
     std::vector<hipEvent_t> tev;            // per-turn timing events (TEV_RING x 7)
     Arena turn_mem;
     hipEvent_t ev[8] = {};
@@ -1205,7 +1206,10 @@ static void engine_step(Engine& E, sb_step_stats* out) {
                            (const uint64_t*)nullptr, 0);
     } else {
         const bool fused = !(E.cfg.flags & 4);
-        unsigned long long* krange = topk_range_reset(E.topk, E.s, fused, (E.cfg.flags & 8) != 0);
+        // the gather's per-pts first-rank table reset by the same launch (the last turn's was read back in
+        // launch_front, ahead on the stream)
+        unsigned long long* krange = topk_range_reset(E.topk, E.s, fused, (E.cfg.flags & 8) != 0, E.d_small + 8);
+        E.first_reset = true;
         unsigned long long* fh = topk_fused_hist(E.topk);
         const uint64_t* fb = topk_fused_base(E.topk);
 #ifndef SB_EMIT_GRID
@@ -1271,7 +1275,8 @@ static void finish_turn(Engine& E, int64_t nu, bool heur, bool desc, const doubl
     nt.hi = (uint64_t*)E.turn_mem.alloc(m * 8);
     nt.par = (uint32_t*)E.turn_mem.alloc(m * 4);
     nt.n = m;
-    SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
+    if (!E.first_reset) SB_HIP(hipMemsetAsync(E.d_small + 8, 0xFF, 256 * 4, E.s));
+    E.first_reset = false;
 #ifndef SB_GATHER_GRID
 #define SB_GATHER_GRID 4096   // blocks of the descriptor gather (each thread walks m / (256 * grid) kept states)
 #endif

@@ -128,7 +128,9 @@ struct TopkScratch {
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
                          hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false,
                          const uint32_t* payload = nullptr, bool full_key = false);
-unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false);
+// fill_ff (optional): 256 u32 words set to ~0 by the same launch (the gather's per-pts first-rank table)
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false,
+                                     uint32_t* fill_ff = nullptr);
 unsigned long long* topk_fused_hist(TopkScratch& s);
 const uint64_t* topk_fused_base(TopkScratch& s);
 // size the scratch for n keys and keep kept (avoids allocation on the step path)

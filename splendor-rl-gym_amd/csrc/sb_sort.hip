@@ -1193,7 +1193,8 @@ void TopkScratch::release() {
 // before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
 // first-pass window (from the previous turn's maximum: its top bin sits 64 bins (two binades) above
 // it) and zero the histogram the producer adds to
-__global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window) {
+__global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window, uint32_t* fill_ff) {
+    if (fill_ff) fill_ff[threadIdx.x] = 0xFFFFFFFFu;   // the caller's 256-word table (the gather's first ranks)
     if (threadIdx.x == 0) {
         if (fused) {
             const int64_t top = (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
@@ -1232,9 +1233,9 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     }
 }
 
-unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window) {
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window, uint32_t* fill_ff) {
     s.small.ensure(ST_WORDS);
-    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(256), 0, st, s.small.p, (int)fused, (int)off_window);
+    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(256), 0, st, s.small.p, (int)fused, (int)off_window, fill_ff);
     return (unsigned long long*)(s.small.p + ST_MIN);
 }
 
