@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 3, session 5: the whole -m gpu suite on the final tree (payload copy folded into the fix-up kernels,
 # sort setup folded into the final partition's scan), smoke, the driver's bench command, then one kernel trace
-O=${1:-gpurun_out/s5p}; mkdir -p $O
+O=${1:-gpurun_out/s5q}; mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
