@@ -64,7 +64,9 @@ typedef struct {
                                   load instead of 60% (exercises rebuilds of large tables); bit 5: sharded record
                                   buffers for 48 raw children per parent instead of the worst case (several
                                   ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY); bit 6: reserved (set by
-                                  the host when it expands with sbd_expand_parts) */
+                                  the host when it expands with sbd_expand_parts); bit 7 (test): the key
+                                  pass gives every key to rank 0 (parts that send no records; results
+                                  unchanged) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;

@@ -44,7 +44,32 @@ def to_signed(k: int) -> int:
     return k - (1 << 64) if k >= (1 << 63) else k
 
 
+def check_cards(cards) -> None:
+    """The packed form holds a card SET; refuse a ``cards`` tuple it would silently change.
+
+    The reference keeps ``cards`` as a tuple built by ``insort`` (src/solver.py:343), hashes that tuple
+    (:318) and never checks ownership in ``buy_card`` (:338-355).  A tuple with an id outside 0..89, a
+    repeated id or ids out of order would be re-ordered / collapsed / mis-packed here, giving a different
+    key and a different search: those roots are refused instead."""
+    prev = -1
+    for c in cards:
+        if type(c) is not int and not hasattr(c, '__index__'):
+            raise TypeError(f'card id {c!r} is not an int')
+        c = int(c)
+        if not 0 <= c < 90:
+            raise ValueError(f'card id {c} outside the deck (0..89): the packed state cannot hold it')
+        if c == prev:
+            raise ValueError(f'card {c} appears twice in cards: the packed state holds a card set')
+        if c < prev:
+            raise ValueError(f'cards {tuple(cards)} are not in ascending order (the reference keeps them '
+                             'sorted with insort): the packed state would hash a different tuple')
+        prev = c
+
+
 def encode(cards, gems, pts: int, saved: int) -> tuple[int, int]:
+    check_cards(cards)
+    if len(gems) != COLOR_NUM:
+        raise ValueError(f'gems must have {COLOR_NUM} counts: {gems}')
     lo = 0
     hi = 0
     for c in cards:

@@ -482,6 +482,11 @@ class DistSolve:
                 ret = b.answer_buffer(cap)
                 self._mark(st, 'expand')
             from_src = M[:, me]                               # records each source sends me in this part
+            if ans_base + int(from_src.sum()) > cap:
+                # the receive bound is an estimate (max raw ratio so far + 50%), not a worst case
+                raise RuntimeError(f'sharded dedup: {ans_base + int(from_src.sum())} records received this turn '
+                                   f'exceed the receive bound {cap} estimated from the raw ratio so far '
+                                   '(sbd_expand_parts lostb_cap): capacity estimate exceeded, not out of memory')
             ostart = np.concatenate([[0], np.cumsum(cnt)])
             with ctx():
                 key = b.part_pack(j, int(ostart[-1]), send_base)
@@ -734,7 +739,7 @@ class HipBackend:
         torch.cuda.set_device(self.device)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 48) | (64 if self.KEYPASS and world > 1 else 0),
+                         flags=2 | (int(extra_flags) & 176) | (64 if self.KEYPASS and world > 1 else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))

@@ -112,6 +112,19 @@ class State:
     def packed(self) -> tuple[int, int]:
         return codec.encode(self.cards, self.gems, self.pts, self.saved)
 
+    def _packed_checked(self) -> tuple[int, int]:
+        """The packed form of a state the engine can expand exactly as the reference would.  The packed
+        form derives ``bonus`` from the card set; the reference's ``State(cards, bonus, ...)``
+        (src/solver.py:308-318) keeps ``bonus`` as given, and a hand-made one (a head-start bonus, an
+        edited field) would expand and score differently: refused, as are card tuples the packed form
+        cannot hold (codec.check_cards)."""
+        lo, hi = self.packed()
+        derived = codec.decode(lo, hi)[1]
+        if tuple(self.bonus) != derived:
+            raise ValueError(f'State.bonus {tuple(self.bonus)} differs from the bonus implied by State.cards '
+                             f'{derived}: the engine derives bonus from the cards and cannot hold a different one')
+        return lo, hi
+
     def __repr__(self):
         if self.cards:
             return f'{self.gems!r} {"-".join(str(deck[c]) for c in self.cards)}'
@@ -141,10 +154,7 @@ class State:
         The packed form keeps ``bonus`` implied by ``cards``; states whose ``bonus``
         or ``gems`` were edited by hand are re-packed from their fields.
         """
-        lo, hi = self.packed()
-        derived_bonus = codec.decode(lo, hi)[1]
-        if tuple(self.bonus) != derived_bonus:
-            raise ValueError('State.bonus must equal the bonus implied by State.cards for device expansion')
+        lo, hi = self._packed_checked()
         (clo, chi, _), = device_successors([lo], [hi])
         for a, b in zip(clo.tolist(), chi.tolist()):
             yield State.from_packed(a, b)
@@ -164,6 +174,16 @@ class State:
         ``device + gpus - 1``), one worker process each (``multi.launch``); same
         output, same path, same ``random`` state afterwards.
         """
+        # everything that can refuse the call is checked before the banner is printed
+        heuristic = HEURISTICS.get(heuristic_name, simple_heuristic)
+        host_scored = use_heuristic and heuristic not in _BUILTIN_IDS
+        if gpus > 1 and host_scored:
+            raise ValueError('a user-registered heuristic scores on the host: solve it with gpus=1')
+        lo, hi = self._packed_checked()
+        if self.hash != hash((self.cards, self.gems)):
+            # the reference seeds its trail with this object (src/solver.py:426), i.e. under its stale hash
+            raise ValueError('State fields were edited after construction (its hash is stale): the reference '
+                             "would seed the trail with the stale hash; build the root with State(...) instead")
         if verbose:
             print('=' * 60)
             print('SPEEDRUN MODE SOLVER')
@@ -176,18 +196,14 @@ class State:
             print('Card Visibility: All 90 cards')
             print('=' * 60)
             print()
-        heuristic = HEURISTICS.get(heuristic_name, simple_heuristic)
         hid = _BUILTIN_IDS.get(heuristic, 0) if use_heuristic else 0
-        if use_heuristic and heuristic not in _BUILTIN_IDS:
+        if host_scored:
             # a user-registered callable (HEURISTICS.md:204-229): the device expands and dedups; the callable
             # scores next_queue on the host, in next_queue order (the order `sorted` calls its key in, so it
             # consumes `random` exactly as the reference); the device runs the stable top-k of its scores
             hid = L.SB_HEUR_HOST
         st = random.getstate()
-        lo, hi = self.packed()
         if gpus > 1:
-            if hid == L.SB_HEUR_HOST:
-                raise ValueError('a user-registered heuristic scores on the host: solve it with gpus=1')
             from .multi import launch
             res = launch({'goal': goal_pts, 'use_heuristic': bool(use_heuristic), 'heuristic': hid,
                           'beam_width': beam_width, 'mt': list(st[1]), 'root': [lo, hi], 'verbose': verbose,

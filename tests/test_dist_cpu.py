@@ -47,23 +47,28 @@ def _worker(rank, world, port, cfg, outdir):
     st = random.getstate()[1]
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
     b.parts = cfg.get('parts', 0)   # > 0: the pipelined protocol (the HIP key pass's exchange parts)
-    comm = Comm(torch.device('cpu'))
+    if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
+        from deferred_comm import DeferredComm
+        comm = DeferredComm(torch.device('cpu'))
+    else:
+        comm = Comm(torch.device('cpu'))
     if cfg.get('serialize'):   # the profiling wrappers (bench_dist.py SB_DIST_SERIALIZE=1) change nothing
         from splendor_amd.dist import SerializedBackend
         b = SerializedBackend(b)
         comm.devlock = b.lock
     solve = DistSolve(b, comm, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                       beam_width=cfg['width'])
-    if cfg.get('toggle'):   # bench.py's window edges: the next turn's expansion deferred to the next step
-        trace = []
-        while not solve.done:
+    trace = []
+    while not solve.done:
+        if cfg.get('toggle'):   # bench.py's window edges: the next turn's expansion deferred to the next step
             solve.lookahead = len(trace) % 3 != 1
-            trace.append(solve.step())
-    else:
-        trace = solve.run()
+        trace.append(solve.step())
+        if cfg.get('deferred'):
+            assert not comm.outstanding, f'step {len(trace)} left an all_to_all handle unwaited'
     out = {'trace': trace, 'counts': [c.tolist() for c in solve.counts], 'path': [list(x) for x in solve.path()],
            'slices': [[lo, hi, par] for lo, hi, par in b.turns],
-           'mt': b.mt_state().tolist() if cfg['heur'] else None}
+           'mt': b.mt_state().tolist() if cfg['heur'] else None,
+           'deferred': [comm.deferred_calls, comm.waits] if cfg.get('deferred') else None}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     dist.destroy_process_group()
@@ -98,6 +103,15 @@ CASES = [
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'parts': 4}),
     (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'serialize': True,
          'parts': 2}),
+    # Comm's RCCL branches under RCCL's completion contract (deferred receive buffers, poisoned until
+    # wait): the pipelined protocol at worlds 2/4/8 and the chunked legacy exchange
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'deferred': True}),
+    (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'parts': 4, 'deferred': True}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'parts': 2,
+         'deferred': True}),
+    (4, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'chunks': 3,
+         'deferred': True}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'parts': 2, 'deferred': True}),
 ]
 
 
@@ -128,4 +142,6 @@ def test_sharded_solve_matches_oracle(world, cfg):
     assert all([tuple(p) for p in r['path']] == path for r in res)
     if cfg['heur']:
         assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    if cfg.get('deferred'):   # the deferred path really ran: every rank issued async exchanges and waited for each
+        assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), [r['deferred'] for r in res]
     o.close()

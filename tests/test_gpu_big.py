@@ -2,7 +2,7 @@
 the pinned C oracle (oracle/make_big_golden.py; the Python reference cannot run these widths here):
 
   * C4: realistic 2 players, goal 15, shuffled market seed 0, W=1M, one GPU
-  * the sharded protocol at W=4M: world 1 (flags bit 1) on C3 (balanced), and world 2 on one GPU (gloo
+  * the sharded protocol at W=4M: world 1 (flags bit 1) on C3 (balanced; over gloo and over RCCL), and world 2 on one GPU (gloo
     transport, HIP per-rank primitives) on C5's heuristic (efficiency) — every turn's beam digest over the
     rank slices in rank order, turn sizes, path and final MT state
   * C5 itself (goal 15, efficiency, W=32M): the single-GPU engine (queues of >= 2^24 parents: 8-byte
@@ -79,7 +79,14 @@ def _worker(rank, world, port, cfg, outdir):
     from splendor_amd.engine import HEURISTIC_IDS
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    backend = cfg.get('backend', 'gloo')
+    if backend == 'nccl':   # RCCL: one rank per GPU (a world of one here), device bound at init as bench_dist does
+        import torch
+        torch.cuda.set_device(0)
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', 0))
+    else:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+    assert dist.get_backend() == backend
     random.seed(cfg['seed'])
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=True,
                    heuristic=HEURISTIC_IDS[cfg['heuristic']], beam_width=cfg['width'],
@@ -108,11 +115,16 @@ def _worker(rank, world, port, cfg, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,name', [(1, 'oracle_g15_balanced_w4000000_s0.json'),
-                                        (2, 'oracle_g15_efficiency_w4000000_s0.json')])
-def test_sharded_w4m_oracle_golden(world, name):
+@pytest.mark.parametrize('world,name,backend', [(1, 'oracle_g15_balanced_w4000000_s0.json', 'gloo'),
+                                                (1, 'oracle_g15_balanced_w4000000_s0.json', 'nccl'),
+                                                (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo')])
+def test_sharded_w4m_oracle_golden(world, name, backend):
+    """The sharded protocol at W=4M.  The nccl case is the C3 solve as `bench.py --gpus 1` with SB_FORCE_DIST=1
+    runs it: init_process_group('nccl', device_id=...), the engine on torch's stream (sbd_set_stream) and
+    Comm's RCCL branches (a world of one: RCCL refuses two ranks on one GPU)."""
     g = golden(name)
-    cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed']}
+    cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
+           'backend': backend}
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]

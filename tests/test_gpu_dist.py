@@ -52,7 +52,8 @@ def _worker(rank, world, port, cfg, outdir):
     random.seed(cfg['seed'])
     st = random.getstate()[1]
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
-                   heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st, visited_log2=cfg.get('vlog2', 0))
+                   heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st, visited_log2=cfg.get('vlog2', 0),
+                   extra_flags=cfg.get('flags', 0))
     solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
     trace = solve.run()
     slices = []
@@ -87,6 +88,10 @@ CASES = [
     # the pipelined key pass in one part, and in 16 (parts of a few chunks, some empty on small turns)
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'parts': 1}),
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'parts': 16}),
+    # every key owned by rank 0 (flags bit 7): rank 0's parts send no records, so the apply must see its own
+    # children marked (k_keys_b runs without a send buffer), never a previous turn's record positions
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 128}),
+    (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 128, 'parts': 3}),
 ]
 
 

@@ -126,3 +126,62 @@ def test_custom_heuristic_routes_to_host_scored_engine(monkeypatch):
         monkeypatch.setitem(HEURISTICS, 'mine', lambda s: 1.0)
         with pytest.raises(_lib.SplendorBeamError):
             State.newgame().solve(goal_pts=3, use_heuristic=True, heuristic_name='mine', verbose=False)
+
+
+def _root(cards, bonus=None, gems=(0, 0, 0, 0, 0), pts=0, saved=0):
+    if bonus is None:
+        b = [0] * 5
+        for c in cards:
+            b[deck[c].bonus.value] += 1
+        bonus = tuple(b)
+    return State(tuple(cards), tuple(bonus), tuple(gems), pts, saved)
+
+
+@pytest.mark.parametrize('make,match', [
+    # head-start bonus not implied by the cards (the reference keeps bonus as given, src/solver.py:308-318)
+    (lambda: _root((), bonus=(1, 0, 0, 0, 0)), 'bonus'),
+    (lambda: _root((5, 21, 40), bonus=(2, 1, 0, 0, 1)), 'bonus'),
+    # duplicate card (buy_card has no ownership check, src/solver.py:338-355)
+    (lambda: State.newgame().buy_card(7).buy_card(7), 'twice'),
+    # card ids outside the deck
+    (lambda: _root((90,), bonus=(0,) * 5), 'outside'),
+    (lambda: _root((-1,), bonus=(0,) * 5), 'outside'),
+    # an unsorted tuple hashes differently from the sorted card set
+    (lambda: State((21, 5), (1, 1, 0, 0, 0), (0,) * 5, 0, 0), 'ascending'),
+])
+def test_solve_refuses_roots_the_packed_state_cannot_hold(make, match, capsys):
+    """No root the reference would solve gives a different path without an error: each
+    such root raises before the banner, with or without a GPU."""
+    st = make()
+    with pytest.raises(ValueError, match=match):
+        st.solve(goal_pts=3, use_heuristic=True, heuristic_name='simple', beam_width=10)
+    assert capsys.readouterr().out == ''
+
+
+def test_solve_refuses_stale_hash_root(capsys):
+    """The reference's mutated fixture (tests/test_solver.py:6-12): gems edited after construction leave a
+    stale hash, which the reference's trail would be seeded with (src/solver.py:426)."""
+    st = State.newgame()
+    for card in (40, 5, 21):
+        st = st.buy_card(card)
+    st.gems = (1, 2, 0, 0, 3)
+    with pytest.raises(ValueError, match='stale'):
+        st.solve(goal_pts=3, verbose=True)
+    assert capsys.readouterr().out == ''
+    fresh = State(st.cards, st.bonus, st.gems, st.pts, st.saved)
+    assert fresh._packed_checked() == codec.encode((5, 21, 40), (1, 2, 0, 0, 3), st.pts, st.saved)
+
+
+def test_gpus_with_host_heuristic_refused_before_banner(monkeypatch, capsys):
+    monkeypatch.setitem(HEURISTICS, 'mine', lambda s: 1.0)
+    with pytest.raises(ValueError, match='gpus=1'):
+        State.newgame().solve(goal_pts=3, use_heuristic=True, heuristic_name='mine', gpus=2)
+    assert capsys.readouterr().out == ''
+
+
+def test_codec_check_cards():
+    codec.check_cards(())
+    codec.check_cards((0, 1, 89))
+    for bad in ((3, 3), (2, 1), (90,), (-1,)):
+        with pytest.raises(ValueError):
+            codec.check_cards(bad)
