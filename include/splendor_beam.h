@@ -65,8 +65,9 @@ typedef struct {
                                   buffers for 48 raw children per parent instead of the worst case (several
                                   ranks sharing one GPU), overflow fails the step (SB_ERR_CAPACITY); bit 6: reserved (set by
                                   the host when it expands with sbd_expand_parts); bit 7 (test): the key
-                                  pass gives every key to rank 0 (parts that send no records; results
-                                  unchanged) */
+                                  pass gives every key (with bit 8: every card set) to rank 0 (parts that
+                                  send no records; results unchanged); bit 8: card-set ownership of the
+                                  sharded trail (sbd_mig_*, world_size > 1) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -310,6 +311,28 @@ int sbd_pack_kept(sb_engine* e, uint64_t* d_rec);
 /* the new slice: n received 4-word records (global next_queue order), stable-sorted by score if heur */
 int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);
 int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
+
+/* ---- card-set ownership of the sharded trail (flags bit 8, world_size > 1; csrc/sb_mig.inc).  Replaces the
+ * key-owner dedup of one step (src/solver.py:446-450 over the global queue): the trail is sharded by the
+ * state's card set, every parent is expanded on the rank owning its card set, so its takes (same cards) are
+ * claimed there and only buys to other card-set owners become records; tags carry the global parent rank.
+ *   range side:  sbd_mig_launch (after the slice arrives, no wait: owner digits, partition counts, the goal
+ *                table copied ahead), sbd_mig_counts (waits: parents per owner), sbd_mig_pack (the slice as
+ *                (lo, hi, global rank) rows grouped by owner, n x 3 u64), all_to_all by the caller
+ *   expand side: sbd_mig_expand (the received rows, source-major, become the expand list; key pass in
+ *                nparts parts), then per part sbd_part_counts / sbd_part_pack (records as (key, tag) pairs,
+ *                two u64 each) / all_to_all / sbd_mig_claim on the owner (answer indices ans_base..),
+ *                sbd_owner_total + sbd_owner_finish, answer bits back, sbd_mig_apply (survivor masks of the
+ *                expand list, n_exp x 3 u64, rows in receive order), all_to_all back
+ *   range side:  sbd_mig_place (masks into slice order, counts, offsets; unique count on the device), then
+ *                sbd_apply_finish / sbd_emit / ... as in the key-owner protocol. */
+int sbd_mig_launch(sb_engine* e, int32_t world);
+int sbd_mig_counts(sb_engine* e, int64_t* counts);
+int sbd_mig_pack(sb_engine* e, int64_t goff, uint64_t* d_rows);
+int sbd_mig_expand(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const uint64_t* d_rows, int64_t n_exp);
+int sbd_mig_claim(sb_engine* e, const uint64_t* d_rec, int64_t m, int64_t ans_base, uint8_t* d_ret);
+int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint64_t* d_masks);
+int sbd_mig_place(sb_engine* e, const uint64_t* d_rmask, void* n_unique_dev);
 
 /* ---- realistic multi-player mode (MultiPlayerState, src/solver.py:471-860; config C4) ----
  * params = {players (2..4), target_points, len tier1, len tier2, len tier3, infinite_resources (0/1:

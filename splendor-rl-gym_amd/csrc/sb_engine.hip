@@ -886,6 +886,17 @@ struct Engine {
     uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
     hipStream_t s_claim = nullptr;
     DBuf<uint32_t> ks_rdr, ks_sown, ks_cc, ks_tot, ks_pc;
+    // card-set ownership of the sharded dedup (sb_mig.inc, cfg flags bit 8): range side (parents' owner digits,
+    // their rows' send positions, the partition histogram, per-owner counts), expand side (the received parents
+    // as SoA + global ranks, raw counts / offsets), gmap (global rank -> expand index | first received record),
+    // mtag (received records' tags by answer index)
+    bool mig = false, mig_pending = false;
+    int64_t mig_n = 0;
+    DBuf<uint8_t> mdig;
+    DBuf<uint32_t> mpos, mhist, xg, xcnt, xoff, gmap;
+    DBuf<uint64_t> xlo, xhi, mtag;
+    uint32_t* h_mpc = nullptr;
+    hipEvent_t mig_ev = nullptr;
     double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
 
@@ -938,6 +949,7 @@ static void check_err_word(Engine& E) {
     if (e & 16u) throw HipError{hipErrorInvalidValue, "heuristic returned NaN: no stable sort order exists"};
     if (e & 32u) throw HipError{hipErrorLaunchFailure, "top-k sort fix-up: more distinct keys in one prefix run than it holds"};
     if (e & 64u) throw HipError{hipErrorOutOfMemory, "sharded records exceed the compact record buffers (flags bit 5)"};
+    if (e & 128u) throw HipError{hipErrorLaunchFailure, "card-set sharded claims: a displaced record is not where its parent maps"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -1457,6 +1469,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
             if (cfg->rank < 0 || cfg->rank >= cfg->world_size || cfg->world_size > 64)
                 throw HipError{hipErrorInvalidValue, "bad rank / world_size (<= 64)"};
             E.own_mask = cap - 1;
+            E.mig = (cfg->flags & 256) != 0 && cfg->world_size > 1;   // card-set ownership (sb_mig.inc)
             SB_HIP(hipMalloc((void**)&E.own, cap * sizeof(Entry)));
             SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
         }
@@ -1753,6 +1766,18 @@ void sb_destroy(sb_engine* h) {
     E.ks_cc.release();
     E.ks_tot.release();
     E.ks_pc.release();
+    E.mdig.release();
+    E.mpos.release();
+    E.mhist.release();
+    E.xg.release();
+    E.xcnt.release();
+    E.xoff.release();
+    E.gmap.release();
+    E.xlo.release();
+    E.xhi.release();
+    E.mtag.release();
+    if (E.h_mpc) (void)hipHostFree(E.h_mpc);
+    if (E.mig_ev) (void)hipEventDestroy(E.mig_ev);
     if (E.h_pc) (void)hipHostFree(E.h_pc);
     for (auto& e : E.ks_ev)
         if (e) (void)hipEventDestroy(e);

@@ -306,7 +306,9 @@ class DistSolve:
         self.max_pts = 0
         self.winner = None                      # (turn, global rank)
         self.counts = []                        # per turn: per-rank slice sizes
-        self.b.expand_launch(self.c.world, 1)   # runs while the host does the turn sync / goal check (the root)
+        # card-set ownership of the trail (HipBackend.MIG / sb_mig.inc): parents migrate to their card-set owners
+        self.mig = bool(getattr(backend, 'mig', False)) and self.c.world > 1
+        self._launch_front(1)                   # runs while the host does the turn sync / goal check (the root)
         self.lookahead = True                   # step() launches the next turn's expansion before returning
         self._front_deferred = False            # lookahead was off: the next step() launches it
         self._turn_sync()
@@ -314,6 +316,12 @@ class DistSolve:
         self.consumed = 0                       # accepted draws used so far (global)
         self.nchunk = int(os.environ.get('SB_DIST_CHUNKS', '8'))   # key exchange / claim pipeline depth
         self.chunk_min = int(os.environ.get('SB_DIST_CHUNK_MIN', str(1 << 23)))   # fewer raw records: one chunk
+
+    def _launch_front(self, n_global):
+        """The next turn's front half, enqueued without a wait: the expansion (key-owner protocol); with card-set
+        ownership the parents' owner digits and partition counts, which _turn_sync always launches itself."""
+        if not self.mig:
+            self.b.expand_launch(self.c.world, n_global)
 
     def offset(self, turn=None) -> int:
         cnt = self.counts[self.turn if turn is None else turn]
@@ -324,7 +332,14 @@ class DistSolve:
         """Once per turn, one all_gather: every rank's slice size and its first local position per
         pts value, giving the slice offsets and the global first position per pts."""
         gt = self.b.goal_table().astype(np.int64)
-        M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt]), host=True)
+        extra = []
+        if self.mig:   # the slice's parents per card-set owner travel with the turn sync
+            self.b.mig_launch()
+            extra = self.b.mig_counts()
+        M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt, extra]), host=True)
+        if self.mig:
+            self._mig_M = M[:, 257:257 + self.c.world].copy()   # [source][owner] parents
+            M = M[:, :257]
         cnt = M[:, 0].copy()
         offs = np.concatenate([[0], np.cumsum(cnt)[:-1]])
         first = M[:, 1:]
@@ -378,8 +393,10 @@ class DistSolve:
         # other owners are partitioned by owner.  Exchange chunks: claims of chunk j overlap chunk j+1's transfer
         C = self.nchunk if st['n_parents'] * 24 >= self.chunk_min else 1
         if self._front_deferred:
-            b.expand_launch(c.world, st['n_parents'])
+            self._launch_front(st['n_parents'])
             self._front_deferred = False
+        if self.mig:
+            return self._dedup_mig(st, off)
         if c.world == 1 and hasattr(b, 'expand_defer'):
             # one rank: no records, nothing to size, so no wait for the expansion; its raw count comes with
             # the apply's wait below
@@ -457,7 +474,45 @@ class DistSolve:
         self._mark(st, 'dedup_exchange')
         return self._post_dedup(st, all_n, off)
 
+    def _dedup_mig(self, st, off):
+        """Dedup with card-set ownership (sb_mig.inc): the slice's parents go to the ranks owning their card
+        sets (one all_to_all of (lo, hi, global rank) rows), which expand them with the pipelined key pass —
+        takes claimed where they are generated, buys for other card-set owners exchanged as (key, tag)
+        records, tags (turn, global parent rank, move) ordering like the reference's first occurrence
+        (src/solver.py:446-450) — and the survivor masks come back to the slice's rank (one all_to_all), which
+        goes on as in the key-owner protocol (noise, emission, joint select and rebalance unchanged)."""
+        c, b = self.c, self.b
+        me, W = c.rank, c.world
+        M = self._mig_M
+        send_sizes, recv_sizes = M[me], M[:, me]
+        n_loc = int(send_sizes.sum())
+        so = np.concatenate([[0], np.cumsum(send_sizes)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(recv_sizes)]).astype(np.int64)
+        rows = b.mig_pack(off, n_loc)                      # (n_loc, 3): grouped by card-set owner
+        pieces = [rows[int(so[o]):int(so[o + 1])].reshape(-1) for o in range(W)]
+        rflat, hd = c.alltoall_pieces(pieces, recv_sizes * 3)
+        c.wait(hd)
+        n_exp = int(ro[-1])
+        b.mig_expand(rflat, n_exp, st['n_parents'])
+        self._mark(st, 'migrate')
+        back = self._exchange_parts(st, rec_words=2)
+        masks = b.mig_apply(back)                          # (n_exp, 3): the expand list's survivor masks
+        rmask = b.mask_buffer(n_loc)
+        c.alltoall_into([masks[int(ro[q]):int(ro[q + 1])] for q in range(W)],
+                        [rmask[int(so[o]):int(so[o + 1])] for o in range(W)])
+        all_n = c.gather_dev(b.mig_place(rmask)).astype(np.int64)   # the placement's count: one wait for both
+        b.apply_finish(int(all_n[c.rank]))
+        self._mark(st, 'dedup_exchange')
+        return self._post_dedup(st, all_n, off)
+
     def _dedup_parts(self, st, off):
+        back = self._exchange_parts(st)
+        all_n = self.c.gather_dev(self.b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
+        self.b.apply_finish(int(all_n[self.c.rank]))
+        self._mark(st, 'dedup_exchange')
+        return self._post_dedup(st, all_n, off)
+
+    def _exchange_parts(self, st, rec_words=1):
         """Dedup with the pipelined key pass (b.parts exchange parts of consecutive parents): for each part,
         its records per owner (one host all_gather of the counts), its keys to their owners (all_to_all), and
         the owners' claims of them — on the claim stream, beside the next parts' key pass on the engine
@@ -490,10 +545,13 @@ class DistSolve:
             ostart = np.concatenate([[0], np.cumsum(cnt)])
             with ctx():
                 key = b.part_pack(j, int(ostart[-1]), send_base)
-                pieces = [key[int(ostart[o]):int(ostart[o + 1])] for o in range(W)]
-                rkey, hd = c.alltoall_pieces(pieces, from_src)
+                rw = rec_words
+                pieces = [key[rw * int(ostart[o]):rw * int(ostart[o + 1])] for o in range(W)]
+                rkey, hd = c.alltoall_pieces(pieces, from_src * rw)
                 c.wait(hd)                                    # RCCL: the claim stream waits for the transfer
-                if rkey.numel():
+                if rkey.numel() and rw == 2:                  # (key, tag) records: tags carry the global order
+                    b.mig_claim(rkey, ans_base, ret)
+                elif rkey.numel():
                     starts = np.concatenate([[0], np.cumsum(from_src)[:-1]])
                     b.owner_claim(rkey, starts, ans_base + starts, ret)
             sends.append((cnt, send_base, ostart))
@@ -532,10 +590,7 @@ class DistSolve:
                 segs.append((at, int(cn[o]), sb + int(os_[o])))
                 at += nb(cn[o])
         b.unpack_bits_segs(rbits, segs, back)
-        all_n = c.gather_dev(b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
-        b.apply_finish(int(all_n[c.rank]))
-        self._mark(st, 'dedup_exchange')
-        return self._post_dedup(st, all_n, off)
+        return back
 
     def _post_dedup(self, st, all_n, off):
         """noise, emission, joint select, rebalance and receive of a step (after the dedup exchange)."""
@@ -592,7 +647,7 @@ class DistSolve:
         if self.heur:
             self.noise.background()
         if self.lookahead:
-            b.expand_launch(c.world, K)   # the next turn's expansion (K parents in all) overlaps its goal check
+            self._launch_front(K)   # the next turn's expansion (K parents in all) overlaps its goal check
         else:   # a benchmark's window edge (bench.py): the next step() launches it
             self._front_deferred = True
         self._turn_sync()
@@ -724,6 +779,8 @@ class HipBackend:
 
     # world > 1: the key pass (flags bit 6, sb_keypass.inc) instead of the expansion kernel + owner partition
     KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'
+    # world > 1: card-set ownership of the trail (flags bit 8, sb_mig.inc) instead of key ownership
+    MIG = os.environ.get('SB_DIST_MIG', '0') == '1'
     PARTS = int(os.environ.get('SB_DIST_PARTS', '4'))   # exchange parts of the pipelined key pass (<= 16)
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
@@ -737,9 +794,11 @@ class HipBackend:
         self._bind()
         self.device = torch.device('cuda', device_index)
         torch.cuda.set_device(self.device)
+        self.mig = bool(self.MIG or (int(extra_flags) & 256)) and world > 1
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 176) | (64 if self.KEYPASS and world > 1 else 0),
+                         flags=2 | (int(extra_flags) & 176) | (64 if self.KEYPASS and world > 1 else 0) |
+                         (256 if self.mig else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
@@ -751,7 +810,7 @@ class HipBackend:
         torch.cuda.set_stream(self.stream)
         L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
         # world > 1: the pipelined key pass; received records are claimed on a second stream beside it
-        self.parts = max(1, min(16, self.PARTS)) if (self.KEYPASS and world > 1) else 0
+        self.parts = max(1, min(16, self.PARTS)) if ((self.KEYPASS or self.mig) and world > 1) else 0
         self.cstream = None
         if self.parts:
             self.cstream = torch.cuda.Stream(self.device)
@@ -801,6 +860,13 @@ class HipBackend:
         lib.sbd_pack_kept.argtypes = [vp, vp]
         lib.sbd_receive.argtypes = [vp, vp, i64, i32]
         lib.sbd_mark_done.argtypes = [vp, i64]
+        lib.sbd_mig_launch.argtypes = [vp, i32]
+        lib.sbd_mig_counts.argtypes = [vp, vp]
+        lib.sbd_mig_pack.argtypes = [vp, i64, vp]
+        lib.sbd_mig_expand.argtypes = [vp, i32, i32, i64, vp, i64]
+        lib.sbd_mig_claim.argtypes = [vp, vp, i64, i64, vp]
+        lib.sbd_mig_apply.argtypes = [vp, vp, vp]
+        lib.sbd_mig_place.argtypes = [vp, vp, vp]
         lib._sbd_bound = True
 
     def _chk(self, rc, what):
@@ -879,8 +945,10 @@ class HipBackend:
         return cnt, cap.value
 
     def part_pack(self, j, n, send_base):
-        """Part j's n records in owner groups (on the claim stream: the caller's current stream)."""
-        key = self._empty(max(int(n), 1))[:int(n)]
+        """Part j's n records in owner groups (on the claim stream: the caller's current stream); with card-set
+        ownership each record is a (key, tag) pair, 2n words."""
+        w = 2 if self.mig else 1
+        key = self._empty(max(w * int(n), 1))[:w * int(n)]
         self._chk(self.lib.sbd_part_pack(self.h, int(j), key.data_ptr() if n else None, int(send_base)), 'sbd_part_pack')
         return key
 
@@ -1041,6 +1109,46 @@ class HipBackend:
         rec = torch.empty((max(int(n_rows), 1), 4), dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None), 'sbd_pack_kept')
         return rec
+
+    # ---------------------------------------------------------------- card-set ownership (sb_mig.inc)
+    def mig_launch(self):
+        self._chk(self.lib.sbd_mig_launch(self.h, int(self.world)), 'sbd_mig_launch')
+
+    def mig_counts(self) -> np.ndarray:
+        out = np.zeros(self.world, np.int64)
+        self._chk(self.lib.sbd_mig_counts(self.h, out.ctypes.data), 'sbd_mig_counts')
+        return out
+
+    def mig_pack(self, goff, n):
+        rows = torch.empty((max(int(n), 1), 3), dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_mig_pack(self.h, int(goff), rows.data_ptr() if n else None), 'sbd_mig_pack')
+        return rows[:int(n)]
+
+    def mig_expand(self, rflat, n_exp, n_global):
+        self.world_x = self.world
+        self._chk(self.lib.sbd_mig_expand(self.h, int(self.world), int(self.parts), int(n_global),
+                                          rflat.data_ptr() if n_exp else None, int(n_exp)), 'sbd_mig_expand')
+        self.n_exp = int(n_exp)
+
+    def mig_claim(self, rrec, ans_base, ret):
+        m = rrec.numel() // 2
+        self._chk(self.lib.sbd_mig_claim(self.h, rrec.data_ptr() if m else None, int(m), int(ans_base),
+                                         ret.data_ptr() if m else None), 'sbd_mig_claim')
+
+    def mask_buffer(self, n):
+        return torch.empty((max(int(n), 1), 3), dtype=torch.int64, device=self.device)[:int(n)]
+
+    def mig_apply(self, back):
+        masks = self.mask_buffer(self.n_exp)
+        self._chk(self.lib.sbd_mig_apply(self.h, back.data_ptr() if back.numel() else None,
+                                         masks.data_ptr() if self.n_exp else None), 'sbd_mig_apply')
+        return masks
+
+    def mig_place(self, rmask):
+        n = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_mig_place(self.h, rmask.data_ptr() if rmask.numel() else None, n.data_ptr()),
+                  'sbd_mig_place')
+        return n
 
     def receive(self, rec, heur):
         self._chk(self.lib.sbd_receive(self.h, rec.data_ptr() if rec.numel() else None, rec.shape[0], int(bool(heur))),

@@ -47,6 +47,9 @@ def _worker(rank, world, port, cfg, outdir):
     st = random.getstate()[1]
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
     b.parts = cfg.get('parts', 0)   # > 0: the pipelined protocol (the HIP key pass's exchange parts)
+    if cfg.get('mig'):   # card-set ownership of the trail (sb_mig.inc restated); 'force0': every card set to rank 0
+        b.mig, b.force0 = True, cfg.get('force0', False)
+        b.parts = b.parts or 2
     if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
         from deferred_comm import DeferredComm
         comm = DeferredComm(torch.device('cpu'))
@@ -112,6 +115,16 @@ CASES = [
     (4, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'chunks': 3,
          'deferred': True}),
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'parts': 2, 'deferred': True}),
+    # card-set ownership: parents migrate to their card-set owners, takes claimed there, buys exchanged as
+    # (key, tag) records; the survivor masks come back to the slice's rank
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'mig': True}),
+    (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True, 'mig': True, 'parts': 3}),
+    (4, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'mig': True,
+         'deferred': True}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'mig': True, 'parts': 1}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'mig': True}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'mig': True}),
+    (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'mig': True, 'force0': True}),
 ]
 
 

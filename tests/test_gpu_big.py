@@ -115,16 +115,17 @@ def _worker(rank, world, port, cfg, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,name,backend', [(1, 'oracle_g15_balanced_w4000000_s0.json', 'gloo'),
-                                                (1, 'oracle_g15_balanced_w4000000_s0.json', 'nccl'),
-                                                (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo')])
-def test_sharded_w4m_oracle_golden(world, name, backend):
+@pytest.mark.parametrize('world,name,backend,flags', [(1, 'oracle_g15_balanced_w4000000_s0.json', 'gloo', 0),
+                                                      (1, 'oracle_g15_balanced_w4000000_s0.json', 'nccl', 0),
+                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo', 0),
+                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo', 256)])
+def test_sharded_w4m_oracle_golden(world, name, backend, flags):
     """The sharded protocol at W=4M.  The nccl case is the C3 solve as `bench.py --gpus 1` with SB_FORCE_DIST=1
     runs it: init_process_group('nccl', device_id=...), the engine on torch's stream (sbd_set_stream) and
     Comm's RCCL branches (a world of one: RCCL refuses two ranks on one GPU)."""
     g = golden(name)
     cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
-           'backend': backend}
+           'backend': backend, 'flags': flags}   # flags 256: card-set ownership of the trail (sb_mig.inc)
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
@@ -180,7 +181,8 @@ def test_c5_w32m_single_gpu_oracle_golden():
 
 
 @pytest.mark.skipif(not golden_exists(C5), reason='C5 golden not generated')
-def test_c5_sharded_world8_oracle_golden():
+@pytest.mark.parametrize('mig', [False, True])
+def test_c5_sharded_world8_oracle_golden(mig):
     """C5 as the 8-GPU job runs it, 8 ranks on one GPU (gloo transport, HIP per-rank primitives, 4M
     states per rank): every turn's digest over the rank slices, sizes, path, final MT state on every
     rank; each rank's owner shard starts at 2^28 slots and is rebuilt on the way; record buffers sized for
@@ -188,7 +190,8 @@ def test_c5_sharded_world8_oracle_golden():
     g = golden(C5)
     world = 8
     cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
-           'visited_log2': 28, 'digest_inline': True, 'flags': 32}   # 8 ranks share one GPU's HBM
+           'visited_log2': 28, 'digest_inline': True,
+           'flags': 32 | (256 if mig else 0)}   # 8 ranks share one GPU's HBM; 256: card-set ownership
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]

@@ -92,6 +92,18 @@ CASES = [
     # children marked (k_keys_b runs without a send buffer), never a previous turn's record positions
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 128}),
     (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 128, 'parts': 3}),
+    # card-set ownership of the trail (flags bit 8, sb_mig.inc): parents migrate to their card-set owners,
+    # takes are claimed where generated, buys exchanged as (key, tag) records, masks back to the slice's rank
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'flags': 256}),
+    (3, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 256}),
+    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'flags': 256}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'flags': 256}),
+    (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1, 'flags': 256,
+         'parts': 1}),
+    (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'flags': 256, 'parts': 16}),
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10, 'flags': 256}),
+    # every card set owned by rank 0: the other ranks expand nothing, rank 0 sends no records
+    (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 384}),
 ]
 
 
