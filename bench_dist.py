@@ -21,6 +21,37 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 
 
+def keypass_pmc(kernel):
+    """HBM bytes per step of the world > 1 key kernel (k_mkeys_a / k_keys_a) from the newest committed world-2
+    serialised PMC summary (profiles/r*_w2_pmc.json, profiles/pmc_sharded.py), or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_w2_pmc.json')), reverse=True):
+        try:
+            v = json.load(open(f))['pmc'][kernel]
+            return {'hbm_bytes_per_step': int(v['hbm_bytes_per_step']), 'device_ms_per_step': v['device_ms_per_step'],
+                    'l2_hit_rate': v.get('tcc_hit_rate'),
+                    'source': os.path.relpath(f, REPO) + ' (world 2 on one GPU, serialised ranks; rocprofv3 --pmc '
+                              'FETCH_SIZE / WRITE_SIZE / TCC_HIT,MISS, separate passes; hbm = 2 FETCH + WRITE)'}
+        except (KeyError, ValueError, OSError):
+            continue
+    return None
+
+
+def carried_cpu_baseline():
+    """The N=1 cpu_baseline measured by bench.py on a GPU box (profiles/r*_cpu_baseline_n1.json), carried on
+    the N > 1 lines so every line has the CPU reference beside it (it is not re-timed there: the contract
+    times it at N=1 only)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_cpu_baseline_n1.json')), reverse=True):
+        try:
+            d = json.load(open(f))
+            d['carried_from'] = os.path.relpath(f, REPO) + ' (measured at N=1 by bench.py on a GPU box host)'
+            return d
+        except (ValueError, OSError):
+            continue
+    return None
+
+
 def sharded_pmc():
     """k_expand<true> (the sharded step's dominant kernel: own claims + records) from the newest committed
     sharded PMC summary (profiles/r*_profile_sharded_summary.json), or None."""
@@ -41,7 +72,8 @@ def main(args):
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    from bench import GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, probe_window, step_bytes, timed_steps
+    from bench import (GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, expand_bytes, probe_window, step_bytes,
+                       timed_steps)
     from splendor_amd.dist import Comm, DistSolve, HipBackend, SerializedBackend, TimedProxy
     from splendor_amd.engine import HEURISTIC_IDS
     if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
@@ -68,7 +100,8 @@ def main(args):
         b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=GOAL, use_heuristic=True,
                        heuristic=HEURISTIC_IDS[args.heuristic], beam_width=W, mt_state625=random.getstate()[1],
                        visited_log2=int(os.environ.get('SB_VISITED_LOG2', '0')),
-                       extra_flags=int(os.environ.get('SB_DIST_FLAGS', '0')))   # 32: several ranks on one GPU
+                       extra_flags=int(os.environ.get('SB_DIST_FLAGS', '0')) | 1)   # 32: several ranks on one GPU;
+        # 1: key-pass device time per step (the dominant world > 1 kernel's roofline); 256: card-set ownership
         comm = Comm(b.device)
         if serial:   # profiling several ranks on one GPU: each rank's device work alone (SerializedBackend),
             b = SerializedBackend(b)   # gloo's staging copies under the same lock
@@ -124,7 +157,10 @@ def main(args):
             'config': {'workload': f'speedrun goal_pts={GOAL} -u -H {args.heuristic} beam_width={W} '
                                    f'({args.width} per GPU; C5 at 8 GPUs x 4M)',
                        'beam_width': W, 'heuristic': args.heuristic, 'seed': args.seed,
-                       'parallelism': f'beam sharded over {world} GPUs ({backend})',
+                       'parallelism': f'beam sharded over {world} GPUs ({backend}); trail owned by '
+                                      + ('card set (parents migrate to their owners)'
+                                         if world > 1 and (HipBackend.MIG or int(os.environ.get('SB_DIST_FLAGS', '0')) & 256)
+                                         else 'key hash'),
                        'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
                        'timed_turns': [first, first + length - 1], 'moves': turns,
                        'timed_expansions': ('engine lookahead at the window edges: the turn after each segment'
@@ -138,13 +174,39 @@ def main(args):
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},
             'cpu_baseline': None,
         }
-        sh = sharded_pmc()
-        if sh:   # the dominant kernel's HBM bytes per launch, profiled on the sharded path at world 1
-            out['roofline']['traffic'] = sh['hbm_bytes_per_launch']
-            out['roofline']['traffic_kernel'] = sh['kernel']
-            out['roofline']['traffic_source'] = sh['source']
+        kp = [p['keypass_ms'] for p in per if p.get('keypass_ms')]
+        if world > 1 and kp:
+            # the dominant world > 1 kernel: the key pass (k_mkeys_a with card-set ownership, else k_keys_a), its
+            # device time per step from HIP events around its launches on this rank (rank 0), its algorithmic
+            # bytes per rank: 16 B parent + 24 B masks + 21 B per raw child + 16 B per new key (bench.py's
+            # expand_bytes, the single GPU's k_expand model), at the all-rank mean share (raw / world ...)
+            mig_on = HipBackend.MIG or bool(int(os.environ.get('SB_DIST_FLAGS', '0')) & 256)
+            kname = 'k_mkeys_a' if mig_on else 'k_keys_a'
+            kms = sum(kp) / len(kp)
+            abytes = expand_bytes(parents / len(per) / world, raw / len(per) / world, uniq / len(per) / world)
+            ach = abytes / (kms * 1e-3) / 1e9
+            out['roofline'] = {'bound': 'hbm', 'kernel': kname, 'achieved': round(ach, 2), 'peak': HBM_PEAK_GBS,
+                               'unit': 'GB/s', 'frac': round(ach / HBM_PEAK_GBS, 5), 'traffic': None,
+                               'launch_ms': round(kms, 4), 'launches_per_step': int(os.environ.get('SB_DIST_PARTS', '4')),
+                               'algorithmic_bytes_per_step': int(abytes),
+                               'whole_step': {'model': 'SURVEY §8d per GPU', 'achieved': round(gbs / world, 2),
+                                              'frac': round(gbs / world / HBM_PEAK_GBS, 5)}}
+            pm = keypass_pmc(kname)
+            if pm:
+                out['roofline']['traffic'] = pm['hbm_bytes_per_step']
+                out['roofline']['traffic_device_ms'] = round(pm['device_ms_per_step'], 4)
+                out['roofline']['l2_hit_rate'] = pm['l2_hit_rate']
+                out['roofline']['traffic_source'] = pm['source']
+        else:
+            sh = sharded_pmc()
+            if sh:   # the dominant kernel's HBM bytes per launch, profiled on the sharded path at world 1
+                out['roofline']['traffic'] = sh['hbm_bytes_per_launch']
+                out['roofline']['traffic_kernel'] = sh['kernel']
+                out['roofline']['traffic_source'] = sh['source']
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only, after the timed region
             out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, first)
+        elif world > 1:
+            out['cpu_baseline'] = carried_cpu_baseline()
         sys.stdout.flush()
         os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)

@@ -333,6 +333,9 @@ int sbd_mig_expand(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global
 int sbd_mig_claim(sb_engine* e, const uint64_t* d_rec, int64_t m, int64_t ans_base, uint8_t* d_ret);
 int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint64_t* d_masks);
 int sbd_mig_place(sb_engine* e, const uint64_t* d_rmask, void* n_unique_dev);
+/* flags bit 0: device time (ms) of the last pipelined expansion's key kernels (k_keys_a / k_mkeys_a, summed
+ * over its parts; waits for them) — the bench's roofline of the dominant world > 1 kernel */
+int sbd_keypass_ms(sb_engine* e, float* ms);
 
 /* ---- realistic multi-player mode (MultiPlayerState, src/solver.py:471-860; config C4) ----
  * params = {players (2..4), target_points, len tier1, len tier2, len tier3, infinite_resources (0/1:

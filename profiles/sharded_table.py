@@ -16,10 +16,11 @@ import re
 from collections import defaultdict
 
 PHASES = [
-    ('expand', r'^k_expand<true>|^k_keys_a|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
-    ('record pack', r'^k_keys_b'),
+    ('parent migration (card-set owners)', r'^k_mig_digit|^k_mig_unpack|^k_part_scatter<4>|^k_mig_place'),
+    ('expand', r'^k_expand<true>|^k_keys_a|^k_mkeys_a|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
+    ('record pack', r'^k_keys_b|^k_mkeys_b'),
     ('owner partition', r'^k_part_|^k_chunk_counts'),
-    ('owner claims', r'^k_own_'),
+    ('owner claims', r'^k_own_|^k_mig_map|^k_mig_claim'),
     ('answer bits', r'^k_(un)?pack_bits'),
     ('apply', r'^k_apply_w|^k_count_masks|^k_counts_i64|^k_total_i64'),
     ('noise (side stream)', r'^k_mt_'),
@@ -78,7 +79,10 @@ def rank_table(rows, steps, ovl=None):
             if not o:
                 clean[name].append((t1 - t0) / 1e6)
     med = {k: sorted(v)[len(v) // 2] for k, v in clean.items()}
-    ex = [i for i, r in enumerate(rows) if r[0] == 'k_raw_count']   # each step's expansion starts with it
+    # each step's expansion starts with k_raw_count; with card-set ownership its front (the parents' owner
+    # digits, launched at the previous step's end) with k_mig_digit
+    cut = 'k_mig_digit' if any(r[0] == 'k_mig_digit' for r in rows) else 'k_raw_count'
+    ex = [i for i, r in enumerate(rows) if r[0] == cut]
     if len(ex) < steps:
         raise RuntimeError(f'only {len(ex)} expansions in the trace')
     starts = ex[-steps:] + [len(rows)]

@@ -897,6 +897,9 @@ struct Engine {
     DBuf<uint64_t> xlo, xhi, mtag;
     uint32_t* h_mpc = nullptr;
     hipEvent_t mig_ev = nullptr;
+    // sharded key pass timing (flags bit 0): an event pair around each part's key kernel (k_keys_a / k_mkeys_a)
+    hipEvent_t kp_ev[32] = {};
+    int kp_n = 0;
     double htr[3] = {};                   // SB_HOST_TRACE: host times (ms) of the step's sync start / end, emission            // host-scored turn (SB_HEUR_HOST): next_queue size awaiting sb_prune
 };
 
@@ -1778,6 +1781,8 @@ void sb_destroy(sb_engine* h) {
     E.mtag.release();
     if (E.h_mpc) (void)hipHostFree(E.h_mpc);
     if (E.mig_ev) (void)hipEventDestroy(E.mig_ev);
+    for (auto& e : E.kp_ev)
+        if (e) (void)hipEventDestroy(e);
     if (E.h_pc) (void)hipHostFree(E.h_pc);
     for (auto& e : E.ks_ev)
         if (e) (void)hipEventDestroy(e);

@@ -595,6 +595,8 @@ class DistSolve:
     def _post_dedup(self, st, all_n, off):
         """noise, emission, joint select, rebalance and receive of a step (after the dedup exchange)."""
         c, b = self.c, self.b
+        if getattr(b, 'timing', False):   # device time of this step's key kernels (the bench's world > 1 roofline)
+            st['keypass_ms'] = b.keypass_ms()
         k_off = int(all_n[:c.rank].sum())
         N = int(all_n.sum())
         st['n_unique'] = N
@@ -795,9 +797,10 @@ class HipBackend:
         self.device = torch.device('cuda', device_index)
         torch.cuda.set_device(self.device)
         self.mig = bool(self.MIG or (int(extra_flags) & 256)) and world > 1
+        self.timing = bool(int(extra_flags) & 1)   # key-pass device time per step (sbd_keypass_ms)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 176) | (64 if self.KEYPASS and world > 1 else 0) |
+                         flags=2 | (int(extra_flags) & 177) | (64 if self.KEYPASS and world > 1 else 0) |
                          (256 if self.mig else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
@@ -867,6 +870,7 @@ class HipBackend:
         lib.sbd_mig_claim.argtypes = [vp, vp, i64, i64, vp]
         lib.sbd_mig_apply.argtypes = [vp, vp, vp]
         lib.sbd_mig_place.argtypes = [vp, vp, vp]
+        lib.sbd_keypass_ms.argtypes = [vp, vp]
         lib._sbd_bound = True
 
     def _chk(self, rc, what):
@@ -1111,6 +1115,11 @@ class HipBackend:
         return rec
 
     # ---------------------------------------------------------------- card-set ownership (sb_mig.inc)
+    def keypass_ms(self) -> float:
+        out = np.zeros(1, np.float32)
+        self._chk(self.lib.sbd_keypass_ms(self.h, out.ctypes.data), 'sbd_keypass_ms')
+        return float(out[0])
+
     def mig_launch(self):
         self._chk(self.lib.sbd_mig_launch(self.h, int(self.world)), 'sbd_mig_launch')
 
