@@ -495,7 +495,7 @@ class DistSolve:
         n_exp = int(ro[-1])
         b.mig_expand(rflat, n_exp, st['n_parents'])
         self._mark(st, 'migrate')
-        back = self._exchange_parts(st, rec_words=2)
+        back = self._exchange_parts(st, rec_words=3)   # 12-byte records: three int32 (key, parent rank | move)
         masks = b.mig_apply(back)                          # (n_exp, 3): the expand list's survivor masks
         rmask = b.mask_buffer(n_loc)
         c.alltoall_into([masks[int(ro[q]):int(ro[q + 1])] for q in range(W)],
@@ -549,7 +549,7 @@ class DistSolve:
                 pieces = [key[rw * int(ostart[o]):rw * int(ostart[o + 1])] for o in range(W)]
                 rkey, hd = c.alltoall_pieces(pieces, from_src * rw)
                 c.wait(hd)                                    # RCCL: the claim stream waits for the transfer
-                if rkey.numel() and rw == 2:                  # (key, tag) records: tags carry the global order
+                if rkey.numel() and rw == 3:                  # (key, tag) records: tags carry the global order
                     b.mig_claim(rkey, ans_base, ret)
                 elif rkey.numel():
                     starts = np.concatenate([[0], np.cumsum(from_src)[:-1]])
@@ -950,9 +950,11 @@ class HipBackend:
 
     def part_pack(self, j, n, send_base):
         """Part j's n records in owner groups (on the claim stream: the caller's current stream); with card-set
-        ownership each record is a (key, tag) pair, 2n words."""
-        w = 2 if self.mig else 1
-        key = self._empty(max(w * int(n), 1))[:w * int(n)]
+        ownership each record is 12 bytes (key, global parent rank << 7 | move), 3n int32."""
+        if self.mig:   # 12-byte records, three int32 each
+            key = self._empty(max(3 * int(n), 1), torch.int32)[:3 * int(n)]
+        else:
+            key = self._empty(max(int(n), 1))[:int(n)]
         self._chk(self.lib.sbd_part_pack(self.h, int(j), key.data_ptr() if n else None, int(send_base)), 'sbd_part_pack')
         return key
 
@@ -1140,7 +1142,7 @@ class HipBackend:
         self.n_exp = int(n_exp)
 
     def mig_claim(self, rrec, ans_base, ret):
-        m = rrec.numel() // 2
+        m = rrec.numel() // 3
         self._chk(self.lib.sbd_mig_claim(self.h, rrec.data_ptr() if m else None, int(m), int(ans_base),
                                          ret.data_ptr() if m else None), 'sbd_mig_claim')
 
