@@ -316,23 +316,27 @@ int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
  * key-owner dedup of one step (src/solver.py:446-450 over the global queue): the trail is sharded by the
  * state's card set, every parent is expanded on the rank owning its card set, so its takes (same cards) are
  * claimed there and only buys to other card-set owners become records; tags carry the global parent rank.
- *   range side:  sbd_mig_launch (after the slice arrives, no wait: owner digits, partition counts, the goal
- *                table copied ahead), sbd_mig_counts (waits: parents per owner), sbd_mig_pack (the slice as
- *                (lo, hi, global rank) rows grouped by owner, n x 3 u64), all_to_all by the caller
- *   expand side: sbd_mig_expand (the received rows, source-major, become the expand list; key pass in
- *                nparts parts), then per part sbd_part_counts / sbd_part_pack (12-byte records: three u32, the key
- *                and global parent rank << 7 | move; d_key then holds 3 u32 per record) / all_to_all / sbd_mig_claim on the owner (answer indices ans_base..),
- *                sbd_owner_total + sbd_owner_finish, answer bits back, sbd_mig_apply (survivor masks of the
- *                expand list, n_exp x 3 u64, rows in receive order), all_to_all back
- *   range side:  sbd_mig_place (masks into slice order, counts, offsets; unique count on the device), then
- *                sbd_apply_finish / sbd_emit / ... as in the key-owner protocol. */
+ *   range side:  sbd_mig_launch (after the slice arrives, no wait: owner digits and raw child counts, the
+ *                partition counts; the goal table copied ahead), sbd_mig_counts (waits: the slice's parents,
+ *                then its raw children, per owner: 2 x world values), sbd_mig_pack (the slice as (lo, hi,
+ *                global rank) rows grouped by owner, n x 3 u64), all_to_all by the caller
+ *   expand side: sbd_mig_expand (the received rows, source-major, become the expand list; key pass in nparts
+ *                parts), then per part sbd_part_counts / sbd_part_pack (12-byte records: three u32, the key and
+ *                global parent rank << 7 | move) / all_to_all / sbd_mig_claim on the owner (answer indices
+ *                ans_base..), sbd_owner_total + sbd_owner_finish, answer bits back, sbd_mig_apply (the expand
+ *                list's survivors as one bit per raw child in move order, source q's parents in a byte-aligned
+ *                segment of a zeroed stream), all_to_all back
+ *   range side:  sbd_mig_place (the bits into slice order: masks, counts, offsets; unique count on the
+ *                device), then sbd_apply_finish / sbd_emit / ... as in the key-owner protocol. */
 int sbd_mig_launch(sb_engine* e, int32_t world);
 int sbd_mig_counts(sb_engine* e, int64_t* counts);
 int sbd_mig_pack(sb_engine* e, int64_t goff, uint64_t* d_rows);
 int sbd_mig_expand(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const uint64_t* d_rows, int64_t n_exp);
 int sbd_mig_claim(sb_engine* e, const uint32_t* d_rec, int64_t m, int64_t ans_base, uint8_t* d_ret);
-int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint64_t* d_masks);
-int sbd_mig_place(sb_engine* e, const uint64_t* d_rmask, void* n_unique_dev);
+int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint8_t* d_bits, int32_t nseg, const int64_t* seg_start,
+                  const int64_t* seg_byte);
+int sbd_mig_place(sb_engine* e, const uint8_t* d_bits, int32_t nown, const int64_t* group_start,
+                  const int64_t* byte_base, void* n_unique_dev);
 /* flags bit 0: device time (ms) of the last pipelined expansion's key kernels (k_keys_a / k_mkeys_a, summed
  * over its parts; waits for them) — the bench's roofline of the dominant world > 1 kernel */
 int sbd_keypass_ms(sb_engine* e, float* ms);

@@ -893,7 +893,8 @@ struct Engine {
     bool mig = false, mig_pending = false;
     int64_t mig_n = 0;
     DBuf<uint8_t> mdig;
-    DBuf<uint32_t> mpos, mhist, xg, xcnt, xoff, gmap;
+    DBuf<uint32_t> mpos, mhist, xg, xcnt, xoff, gmap, mraw, mrawsend, mrawoff;
+    DBuf<uint64_t> mrawown;
     DBuf<uint64_t> xlo, xhi, mtag;
     uint32_t* h_mpc = nullptr;
     hipEvent_t mig_ev = nullptr;
@@ -1779,6 +1780,10 @@ void sb_destroy(sb_engine* h) {
     E.xlo.release();
     E.xhi.release();
     E.mtag.release();
+    E.mraw.release();
+    E.mrawsend.release();
+    E.mrawoff.release();
+    E.mrawown.release();
     if (E.h_mpc) (void)hipHostFree(E.h_mpc);
     if (E.mig_ev) (void)hipEventDestroy(E.mig_ev);
     for (auto& e : E.kp_ev)

@@ -338,7 +338,9 @@ class DistSolve:
             extra = self.b.mig_counts()
         M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt, extra]), host=True)
         if self.mig:
-            self._mig_M = M[:, 257:257 + self.c.world].copy()   # [source][owner] parents
+            W = self.c.world
+            self._mig_M = M[:, 257:257 + W].copy()            # [source][owner] parents
+            self._mig_R = M[:, 257 + W:257 + 2 * W].copy()    # [source][owner] their raw children
             M = M[:, :257]
         cnt = M[:, 0].copy()
         offs = np.concatenate([[0], np.cumsum(cnt)[:-1]])
@@ -496,11 +498,18 @@ class DistSolve:
         b.mig_expand(rflat, n_exp, st['n_parents'])
         self._mark(st, 'migrate')
         back = self._exchange_parts(st, rec_words=3)   # 12-byte records: three int32 (key, parent rank | move)
-        masks = b.mig_apply(back)                          # (n_exp, 3): the expand list's survivor masks
-        rmask = b.mask_buffer(n_loc)
-        c.alltoall_into([masks[int(ro[q]):int(ro[q + 1])] for q in range(W)],
-                        [rmask[int(so[o]):int(so[o + 1])] for o in range(W)])
-        all_n = c.gather_dev(b.mig_place(rmask)).astype(np.int64)   # the placement's count: one wait for both
+        # survivors back to the range ranks as one bit per raw child (move order), a byte-aligned segment per
+        # (expander, range rank) pair, sized by the raw counts the turn sync carried
+        R = self._mig_R
+        nb = lambda x: (int(x) + 7) // 8
+        sb = np.concatenate([[0], np.cumsum([nb(R[q][me]) for q in range(W)])]).astype(np.int64)
+        rb = np.concatenate([[0], np.cumsum([nb(R[me][o]) for o in range(W)])]).astype(np.int64)
+        bits = b.bits_buffer(int(sb[-1]))
+        b.mig_apply(back, bits, ro, sb[:-1])
+        rbits = b.bits_buffer(int(rb[-1]))
+        c.alltoall_into([bits[int(sb[q]):int(sb[q + 1])] for q in range(W)],
+                        [rbits[int(rb[o]):int(rb[o + 1])] for o in range(W)])
+        all_n = c.gather_dev(b.mig_place(rbits, so, rb[:-1])).astype(np.int64)   # one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
         return self._post_dedup(st, all_n, off)
@@ -868,8 +877,8 @@ class HipBackend:
         lib.sbd_mig_pack.argtypes = [vp, i64, vp]
         lib.sbd_mig_expand.argtypes = [vp, i32, i32, i64, vp, i64]
         lib.sbd_mig_claim.argtypes = [vp, vp, i64, i64, vp]
-        lib.sbd_mig_apply.argtypes = [vp, vp, vp]
-        lib.sbd_mig_place.argtypes = [vp, vp, vp]
+        lib.sbd_mig_apply.argtypes = [vp, vp, vp, i32, vp, vp]
+        lib.sbd_mig_place.argtypes = [vp, vp, i32, vp, vp, vp]
         lib.sbd_keypass_ms.argtypes = [vp, vp]
         lib._sbd_bound = True
 
@@ -1146,19 +1155,23 @@ class HipBackend:
         self._chk(self.lib.sbd_mig_claim(self.h, rrec.data_ptr() if m else None, int(m), int(ans_base),
                                          ret.data_ptr() if m else None), 'sbd_mig_claim')
 
-    def mask_buffer(self, n):
-        return torch.empty((max(int(n), 1), 3), dtype=torch.int64, device=self.device)[:int(n)]
+    def bits_buffer(self, nbytes):
+        """A zeroed byte stream of nbytes plus two words of slack (the kernels touch the word after a segment's
+        last bit); the caller slices [0, nbytes)."""
+        return torch.zeros(((int(nbytes) + 7) // 8 + 2) * 8, dtype=torch.uint8, device=self.device)
 
-    def mig_apply(self, back):
-        masks = self.mask_buffer(self.n_exp)
-        self._chk(self.lib.sbd_mig_apply(self.h, back.data_ptr() if back.numel() else None,
-                                         masks.data_ptr() if self.n_exp else None), 'sbd_mig_apply')
-        return masks
+    def mig_apply(self, back, bits, seg_start, seg_byte):
+        st = np.ascontiguousarray(seg_start, dtype=np.int64)
+        sb = np.ascontiguousarray(seg_byte, dtype=np.int64)
+        self._chk(self.lib.sbd_mig_apply(self.h, back.data_ptr() if back.numel() else None, bits.data_ptr(),
+                                         len(sb), st.ctypes.data, sb.ctypes.data), 'sbd_mig_apply')
 
-    def mig_place(self, rmask):
+    def mig_place(self, rbits, group_start, byte_base):
         n = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self._chk(self.lib.sbd_mig_place(self.h, rmask.data_ptr() if rmask.numel() else None, n.data_ptr()),
-                  'sbd_mig_place')
+        gs = np.ascontiguousarray(group_start, dtype=np.int64)
+        bb = np.ascontiguousarray(byte_base, dtype=np.int64)
+        self._chk(self.lib.sbd_mig_place(self.h, rbits.data_ptr(), len(bb), gs.ctypes.data, bb.ctypes.data,
+                                         n.data_ptr()), 'sbd_mig_place')
         return n
 
     def receive(self, rec, heur):
