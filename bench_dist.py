@@ -169,6 +169,9 @@ def main(args):
                                        if args.engine_stream_end else 'every stream + barrier'),
                        'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh solves)'},
             'value_engine_stream_end': round(parents / el_eng_max, 1),
+            # bytes rank 0 sent to other ranks per timed step, by exchange (Comm.acct; RCCL's own traffic)
+            'exchange_MB_per_step_rank0': {k: round(sum(p.get('xbytes', {}).get(k, 0) for p in per) / len(per) / 1e6, 2)
+                                           for k in sorted({k for p in per for k in p.get('xbytes', {})})},
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},

@@ -57,6 +57,13 @@ class Comm:
         # while the expansion occupies every CU, which a device collective would have to wait for
         self.meta = dist.new_group(backend='gloo') if self.world > 1 else None
         self.devlock = None   # profiling (SerializedBackend.lock): gloo's staging copies under the device lock
+        self.xbytes = {}      # bytes this rank sent to other ranks, per exchange (DistSolve.step hands them out)
+
+    def acct(self, what, nbytes):
+        self.xbytes[what] = self.xbytes.get(what, 0) + int(nbytes)
+
+    def _remote(self, pieces):
+        return sum(int(p.numel()) * p.element_size() for o, p in enumerate(pieces) if o != self.rank)
 
     def _cp(self, fn):
         """A device copy of the gloo staging; under the profiling device lock when one is set."""
@@ -116,16 +123,19 @@ class Comm:
         dist.all_to_all_single(recv, send)
         return recv.cpu().numpy()
 
-    def alltoall(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
+    def alltoall(self, send: torch.Tensor, send_counts, recv_counts, what='other') -> torch.Tensor:
+        row = send.element_size() * (int(send[0].numel()) if send.dim() > 1 and send.shape[0] else 1)
+        self.acct(what, row * (int(sum(send_counts)) - int(send_counts[self.rank])))
         s = self._to(send)
         r = torch.empty((int(sum(recv_counts)),) + tuple(send.shape[1:]), dtype=send.dtype, device=s.device)
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
-    def alltoall_pieces(self, pieces, recv_sizes):
+    def alltoall_pieces(self, pieces, recv_sizes, what='other'):
         """Start an all_to_all of pieces[o] (views, any layout) to rank o; returns (receive buffer,
         handle).  RCCL runs it asynchronously on its own stream; wait(handle) orders this rank's stream
         after it.  gloo (no list all_to_all) packs the pieces and completes at once."""
+        self.acct(what, self._remote(pieces))
         out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=pieces[0].device)
         if self.cpu_coll:
             send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
@@ -136,8 +146,9 @@ class Comm:
         outs = list(out.split([int(x) for x in recv_sizes]))
         return out, dist.all_to_all(outs, list(pieces), async_op=True)
 
-    def alltoall_into(self, pieces, outs):
+    def alltoall_into(self, pieces, outs, what='other'):
         """all_to_all of pieces[o] (views) to rank o, received straight into the views outs[o]."""
+        self.acct(what, self._remote(pieces))
         if self.cpu_coll:
             send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             rows = [int(o.shape[0]) for o in outs]
@@ -156,10 +167,11 @@ class Comm:
         if handle is not None:
             handle.wait()
 
-    def allreduce_tensor(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
+    def allreduce_tensor(self, t: torch.Tensor, op=dist.ReduceOp.SUM, what='select all_reduce'):
         """In-place reduction over ranks of a tensor on this rank's device (no host wait with RCCL)."""
         if self.world == 1:
             return
+        self.acct(what, 2 * (self.world - 1) * t.numel() * t.element_size() // self.world)   # ring volume
         if self.cpu_coll:
             x = self._cp(lambda: t.cpu())
             dist.all_reduce(x, op=op)
@@ -278,7 +290,7 @@ class ShardNoise:
         recv = [cat(x) for x in recv]
         wins = b.noise_pack(cat(send))
         if c.world > 1:
-            wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv])
+            wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv], what='noise windows')
         b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
         self._ahead = A + N + 4 * N   # background() launches the next round below this mark
@@ -379,6 +391,7 @@ class DistSolve:
         c, b = self.c, self.b
         st = {'turn': self.turn, 'records': [], 'done': False}
         self._t = time.perf_counter()
+        c.xbytes.clear()   # this step's exchanges (st['xbytes'], filled at its end)
         cnt = self.counts[self.turn]
         st['n_parents'] = int(cnt.sum())
         if self.done:
@@ -438,7 +451,7 @@ class DistSolve:
             pieces = [send_key[int(ostart[o] + ochunk[j, o]):int(ostart[o] + ochunk[j + 1, o])]
                       for o in range(c.world)]
             if c.world > 1:
-                handles.append(c.alltoall_pieces(pieces, from_src[:, j]))
+                handles.append(c.alltoall_pieces(pieces, from_src[:, j], what='records'))
             else:
                 handles.append((send_key[:0], None))
         n_own = int(src_tot.sum())
@@ -464,7 +477,7 @@ class DistSolve:
                 if src_tot[q]:
                     b.pack_bits(ret[int(src_base[q]):int(src_base[q + 1])], sbits[int(sp[q]):int(sp[q + 1])])
             c.alltoall_into([sbits[int(sp[q]):int(sp[q + 1])] for q in range(c.world)],
-                            [rbits[int(rp[o]):int(rp[o + 1])] for o in range(c.world)])
+                            [rbits[int(rp[o]):int(rp[o + 1])] for o in range(c.world)], what='answer bits')
             back = b.answer_buffer(int(ostart[-1]))
             for o in range(c.world):
                 if own_sz[o]:
@@ -492,7 +505,7 @@ class DistSolve:
         ro = np.concatenate([[0], np.cumsum(recv_sizes)]).astype(np.int64)
         rows = b.mig_pack(off, n_loc)                      # (n_loc, 3): grouped by card-set owner
         pieces = [rows[int(so[o]):int(so[o + 1])].reshape(-1) for o in range(W)]
-        rflat, hd = c.alltoall_pieces(pieces, recv_sizes * 3)
+        rflat, hd = c.alltoall_pieces(pieces, recv_sizes * 3, what='parent rows')
         c.wait(hd)
         n_exp = int(ro[-1])
         b.mig_expand(rflat, n_exp, st['n_parents'])
@@ -508,7 +521,7 @@ class DistSolve:
         b.mig_apply(back, bits, ro, sb[:-1])
         rbits = b.bits_buffer(int(rb[-1]))
         c.alltoall_into([bits[int(sb[q]):int(sb[q + 1])] for q in range(W)],
-                        [rbits[int(rb[o]):int(rb[o + 1])] for o in range(W)])
+                        [rbits[int(rb[o]):int(rb[o + 1])] for o in range(W)], what='survivor bits')
         all_n = c.gather_dev(b.mig_place(rbits, so, rb[:-1])).astype(np.int64)   # one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
@@ -556,7 +569,7 @@ class DistSolve:
                 key = b.part_pack(j, int(ostart[-1]), send_base)
                 rw = rec_words
                 pieces = [key[rw * int(ostart[o]):rw * int(ostart[o + 1])] for o in range(W)]
-                rkey, hd = c.alltoall_pieces(pieces, from_src * rw)
+                rkey, hd = c.alltoall_pieces(pieces, from_src * rw, what='records')
                 c.wait(hd)                                    # RCCL: the claim stream waits for the transfer
                 if rkey.numel() and rw == 3:                  # (key, tag) records: tags carry the global order
                     b.mig_claim(rkey, ans_base, ret)
@@ -590,7 +603,8 @@ class DistSolve:
                 segs.append((ab + int(np.sum(fs[:q])), int(fs[q]), at))
                 at += nb(fs[q])
         b.pack_bits_segs(ret, segs, sbits)
-        c.alltoall_into([sbits[sp[q]:sp[q + 1]] for q in range(W)], [rbits[rp[o]:rp[o + 1]] for o in range(W)])
+        c.alltoall_into([sbits[sp[q]:sp[q + 1]] for q in range(W)], [rbits[rp[o]:rp[o + 1]] for o in range(W)],
+                        what='answer bits')
         back = b.answer_buffer(send_base)
         segs = []
         for o in range(W):
@@ -649,7 +663,7 @@ class DistSolve:
             rrec = torch.empty((int(ro[-1]),) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
             pieces = [rec[int(so[q]):int(so[q + 1])] if q != me else rec[:0] for q in range(c.world)]
             outs = [rrec[int(ro[q]):int(ro[q + 1])] if q != me else rrec[:0] for q in range(c.world)]
-            c.alltoall_into(pieces, outs)
+            c.alltoall_into(pieces, outs, what='kept records')
             rrec[int(ro[me]):int(ro[me + 1])].copy_(rec[int(so[me]):int(so[me + 1])])
         else:
             rrec = rec[:int(dest_counts.sum())]
@@ -663,6 +677,7 @@ class DistSolve:
             self._front_deferred = True
         self._turn_sync()
         self._mark(st, 'rebalance')
+        st['xbytes'] = dict(c.xbytes)
         self.turn += 1
         st['n_kept'] = int(self.counts[-1].sum())
         return st

@@ -36,7 +36,8 @@ class DeferredComm(Comm):
         self.deferred_calls = 0
         self.waits = 0
 
-    def alltoall_pieces(self, pieces, recv_sizes):
+    def alltoall_pieces(self, pieces, recv_sizes, what='other'):
+        self.acct(what, self._remote(pieces))
         snap = [p.clone() for p in pieces]
         send = torch.cat([p.reshape(-1) for p in snap]) if snap else torch.zeros(0)
         data = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype)
@@ -58,7 +59,8 @@ class DeferredComm(Comm):
         self.outstanding.remove(handle)
         self.waits += 1
 
-    def alltoall_into(self, pieces, outs):
+    def alltoall_into(self, pieces, outs, what='other'):
+        self.acct(what, self._remote(pieces))
         send = torch.cat([p.reshape(-1) for p in pieces])
         rows = [int(o.numel()) for o in outs]
         r = torch.empty(sum(rows), dtype=send.dtype)
