@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""N=8 projection of the sharded step from one-GPU measurements.
+
+Inputs: a per-rank phase table (profiles/sharded_table.py --out: serialised world-8 traces on one GPU, each
+rank's kernels alone on the device = its own GPU's device time) and a bench line of the same run
+(bench_dist.py: exchange_MB_per_step_rank0 = bytes rank 0 sent to other ranks per step, by exchange).
+
+Model per rank and step: device time (the table's engine-stream total; the noise side stream overlaps) plus
+the exchanges that sit on the critical path at an effective all_to_all rate B per GPU (xGMI: 7 links per
+MI355X; RCCL's all_to_all rate is unmeasured here — one GPU per box — so B is a parameter), plus a fixed
+latency per collective round.  The records travel in parts beside the key pass, so only their excess over
+the key pass counts; every other exchange counts in full.
+    python3 profiles/project_n8.py TABLE.json BENCH.json [--B 250,400,600] [--lat-us 30] [--rounds 20]
+"""
+import argparse
+import json
+
+OVERLAPPED = {'records'}   # exchanged part by part while the key pass runs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('table')
+    ap.add_argument('bench')
+    ap.add_argument('--B', default='250,400,600', help='effective all_to_all GB/s per GPU')
+    ap.add_argument('--lat-us', type=float, default=30.0, help='latency per collective round (us)')
+    ap.add_argument('--rounds', type=int, default=20, help='collective rounds per step on the critical path')
+    ap.add_argument('--single-ms', type=float, default=4.703, help='one GPU ms/step (BENCH_r03: 4.703)')
+    ap.add_argument('--W', type=float, default=4e6, help='parents per rank')
+    a = ap.parse_args()
+    t = json.load(open(a.table))
+    b = [json.loads(l) for l in open(a.bench) if l.startswith('{')][-1]
+    mean = t['mean_ms']
+    dev = mean['device total (engine stream)']
+    keypass = mean.get('expand', 0.0)
+    x = b.get('exchange_MB_per_step_rank0', {})
+    print(f'device per rank (serialised world-{t["world"]} traces, mean of ranks): {dev:.3f} ms; key pass {keypass:.3f} ms')
+    print('exchange per rank and step (MB sent to other ranks):', {k: round(v, 1) for k, v in x.items()})
+    out = {'device_ms': dev, 'exchange_MB': x, 'projection': []}
+    for B in [float(v) for v in a.B.split(',')]:
+        crit = sum(v for k, v in x.items() if k not in OVERLAPPED) / B          # MB / (GB/s) = ms
+        over = sum(v for k, v in x.items() if k in OVERLAPPED) / B
+        exposed_rec = max(0.0, over - keypass)
+        lat = a.rounds * a.lat_us / 1e3
+        step = dev + crit + exposed_rec + lat
+        gps = 8 * a.W / (step * 1e-3) / 1e9
+        row = {'B_GBps': B, 'critical_exchange_ms': round(crit, 3), 'records_exposed_ms': round(exposed_rec, 3),
+               'latency_ms': round(lat, 3), 'step_ms': round(step, 3), 'G_states_per_s_N8': round(gps, 2),
+               'speedup_vs_1gpu': round(a.single_ms / step * 8, 2)}
+        out['projection'].append(row)
+        print(f'B={B:5.0f} GB/s: step {step:.3f} ms = device {dev:.3f} + exchanges {crit:.3f} (+{exposed_rec:.3f} '
+              f'records beyond the key pass) + latency {lat:.3f} -> {gps:.2f} G states/s at N=8, '
+              f'{row["speedup_vs_1gpu"]:.2f}x one GPU ({a.single_ms} ms)')
+    print(json.dumps(out))
+
+
+if __name__ == '__main__':
+    main()
