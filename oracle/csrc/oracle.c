@@ -508,6 +508,22 @@ static int64_t select_top(const uint64_t* key, int64_t n, int64_t W, uint32_t* o
     return m;
 }
 
+/* Test entry: the speedrun prune as oc_step runs it (select_top, then the stable sort of the W candidates),
+ * as indices into key in kept order; returns the count.  tests/test_oracle.py checks it against a full stable
+ * sort followed by [:W] (the reference's sorted(...)[:beam_width], src/solver.py:452-456). */
+int64_t oc_debug_prune(const uint64_t* key, int64_t n, int64_t W, uint32_t* out) {
+    int64_t k = n < W ? n : W;
+    uint32_t* cand = (uint32_t*)malloc(sizeof(uint32_t) * (k ? k : 1));
+    int64_t nk = select_top(key, n, k, cand);
+    uint64_t* ckey = (uint64_t*)malloc(sizeof(uint64_t) * (nk ? nk : 1));
+    uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (nk ? nk : 1));
+    for (int64_t i = 0; i < nk; i++) ckey[i] = key[cand[i]];
+    sort_desc_stable(ckey, idx, nk);
+    for (int64_t i = 0; i < nk; i++) out[i] = cand[idx[i]];
+    free(cand); free(ckey); free(idx);
+    return nk;
+}
+
 /* One beam step (src/solver.py:434-457). */
 int oc_step(oc_handle* h, oc_stats* out) {
     memset(out, 0, sizeof *out);

@@ -127,3 +127,18 @@ def test_bfs_paths():
         o.run()
         assert [repr(State.from_packed(lo, hi)) for lo, hi in o.path()] == [p[4] for p in g['path']]
         o.close()
+
+
+@pytest.mark.parametrize('seed,n,W,vals', [(0, 5000, 700, 1 << 40), (1, 20000, 19000, 37), (2, 3000, 3000, 5),
+                                            (3, 4096, 1, 2), (4, 10000, 2500, 1 << 62), (5, 1, 1, 10), (6, 7, 100, 3)])
+def test_oracle_prune_equals_stable_sort_slice(seed, n, W, vals):
+    """The oracle's prune (MSB radix select_top of the W-th key, then a stable sort of the candidates: the lean
+    path the C5 golden at W=32M came from) equals a full stable descending sort followed by [:W] —
+    sorted(next_queue, key=..., reverse=True)[:beam_width] (src/solver.py:452-456) — on random keys with heavy
+    ties (few distinct values), full-range keys, W >= n and W = 1."""
+    rng = np.random.default_rng(seed)
+    key = rng.integers(0, vals, n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15 % vals or 1)
+    out = np.zeros(max(min(n, W), 1), np.uint32)
+    k = oracle_c.lib().oc_debug_prune(np.ascontiguousarray(key), n, W, out)
+    ref = sorted(range(n), key=lambda i: int(key[i]), reverse=True)[:W]   # Python's stable sort, as the reference
+    assert k == len(ref) and out[:k].tolist() == ref
