@@ -123,6 +123,8 @@ def cpu_baseline(width, heuristic, seed, first_turn, py_width=300_000):
     dt = time.perf_counter() - t0
     del ps
     out.update(value=round(r['n_parents'] / dt, 1), unit='states/s', cores=1, kind='port',
+               label='pure-Python port of the reference step (about 2-3x the reference\'s own speed: lighter '
+                     'objects; python_reference_quoted below is the reference itself)',
                sample=f'pure-Python restatement of the reference step (oracle/pyref.py, CPython '
                       f'{sys.version.split()[0]}, 1 thread): turn {turn} of the goal-15 -H {heuristic} W={py_width} '
                       f'trajectory (first saturated beam: {r["n_parents"]} parents, {r["n_raw"]} children, '

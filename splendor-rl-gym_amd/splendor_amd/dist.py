@@ -343,10 +343,11 @@ class DistSolve:
     def _turn_sync(self):
         """Once per turn, one all_gather: every rank's slice size and its first local position per
         pts value, giving the slice offsets and the global first position per pts."""
-        gt = self.b.goal_table().astype(np.int64)
         extra = []
-        if self.mig:   # the slice's parents per card-set owner travel with the turn sync
+        if self.mig:   # enqueued first: the goal table's copy rides ahead of it (sbd_goal_table waits for that only)
             self.b.mig_launch()
+        gt = self.b.goal_table().astype(np.int64)
+        if self.mig:   # the slice's parents and raw children per card-set owner travel with the turn sync
             extra = self.b.mig_counts()
         M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt, extra]), host=True)
         if self.mig:
