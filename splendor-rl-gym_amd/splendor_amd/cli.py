@@ -37,7 +37,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument('--seed', help='seed random (and the realistic market shuffle) for a reproducible run',
                    type=int, default=None)
     p.add_argument('--device', help='GPU ordinal (default 0)', type=int, default=0)
-    p.add_argument('--gpus', help='shard the speedrun beam over N GPUs, one process each (default 1)', type=int,
+    p.add_argument('--gpus', help='shard the speedrun beam over N GPUs, one process each (default 1); RCCL between '
+                                  'the GPUs (its asynchronous exchanges are verified with a completion-contract test '
+                                  'double and gloo, not yet on a multi-GPU node: SB_DIST_BACKEND=gloo forces gloo)',
+                   type=int,
                    default=1)
     return p
 
