@@ -192,6 +192,12 @@ __device__ __forceinline__ void tk_pick_body(uint64_t* st) {
     for (int b = t; b < SEL_BINS; b += NT) st[ST_HIST + b] = 0;
 }
 
+#ifndef SB_TK_CAND_PICK
+#define SB_TK_CAND_PICK 0   // candidate passes: SB_TK_CAND_GRID blocks, the last one picks (one launch per pass)
+#endif
+#ifndef SB_TK_CAND_GRID
+#define SB_TK_CAND_GRID 512
+#endif
 #ifndef SB_TK_PICK_FUSED
 #define SB_TK_PICK_FUSED 0   // 1: the select histogram's last block picks (no k_tk_pick launch per pass).  A/B
                              // (profiles/r3/s5/ab_topk.txt): every block's agent-scope release fence writes its
@@ -283,13 +289,15 @@ __global__ __launch_bounds__(256) void k_tk_hsum(const uint32_t* __restrict__ pa
 __global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallback);
 // one select pass: the histogram of the next digit, then the pick (in the histogram's last block, or a launch)
 static void tk_hist_pick(TopkScratch& s, hipStream_t st, const uint64_t* keys, int64_t n, const uint64_t* n_dev,
-                         uint64_t* stv, int only_fallback, unsigned grid) {
+                         uint64_t* stv, int only_fallback, unsigned grid, bool small = false) {
     uint32_t* part = nullptr;
     if (SB_TKH_2STAGE) {
         s.tkh_part.ensure((size_t)grid * SEL_BINS);
         part = s.tkh_part.p;
     }
-    const int fused_pick = SB_TK_PICK_FUSED && !part;
+    // small: a candidate pass (about 0.1M keys on C3) on a small grid whose last block picks — few blocks, so
+    // few of the agent-scope fences that made this slow on the 512-block passes over all keys
+    const int fused_pick = (SB_TK_PICK_FUSED || (small && SB_TK_CAND_PICK)) && !part;
     hipLaunchKernelGGL(k_tk_hist, dim3(grid), dim3(TKH_NT), 0, st, keys, n, n_dev, stv, only_fallback, part, fused_pick);
     if (part)
         hipLaunchKernelGGL(k_tk_hsum, dim3(SEL_BINS / 256, (grid + 31) / 32), dim3(256), 0, st, part, (int)grid, stv,
@@ -1317,7 +1325,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         // remaining digits on the candidates (device-side count; passes after DONE exit at once)
         const uint64_t* nc = stv + ST_NC;
         for (int pass = 0; pass < SEL_PASSES_C; pass++) {
-            tk_hist_pick(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, 512u));
+            tk_hist_pick(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, (unsigned)SB_TK_CAND_GRID), true);
         }
         // candidates above T -> group 2, the first NEED ties -> group 3
         hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
