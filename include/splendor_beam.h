@@ -319,7 +319,7 @@ int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
  *   range side:  sbd_mig_launch (after the slice arrives, no wait: owner digits and raw child counts, the
  *                partition counts; the goal table copied ahead), sbd_mig_counts (waits: the slice's parents,
  *                then its raw children, per owner: 2 x world values), sbd_mig_pack (the slice as (lo, hi,
- *                global rank) rows grouped by owner, n x 3 u64), all_to_all by the caller
+ *                global rank) rows grouped by owner, n x 5 u32), all_to_all by the caller
  *   expand side: sbd_mig_expand (the received rows, source-major, become the expand list; key pass in nparts
  *                parts), then per part sbd_part_counts / sbd_part_pack (12-byte records: three u32, the key and
  *                global parent rank << 7 | move) / all_to_all / sbd_mig_claim on the owner (answer indices
@@ -330,8 +330,8 @@ int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
  *                device), then sbd_apply_finish / sbd_emit / ... as in the key-owner protocol. */
 int sbd_mig_launch(sb_engine* e, int32_t world);
 int sbd_mig_counts(sb_engine* e, int64_t* counts);
-int sbd_mig_pack(sb_engine* e, int64_t goff, uint64_t* d_rows);
-int sbd_mig_expand(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const uint64_t* d_rows, int64_t n_exp);
+int sbd_mig_pack(sb_engine* e, int64_t goff, uint32_t* d_rows);
+int sbd_mig_expand(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const uint32_t* d_rows, int64_t n_exp);
 int sbd_mig_claim(sb_engine* e, const uint32_t* d_rec, int64_t m, int64_t ans_base, uint8_t* d_ret);
 int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint8_t* d_bits, int32_t nseg, const int64_t* seg_start,
                   const int64_t* seg_byte);

@@ -504,9 +504,9 @@ class DistSolve:
         n_loc = int(send_sizes.sum())
         so = np.concatenate([[0], np.cumsum(send_sizes)]).astype(np.int64)
         ro = np.concatenate([[0], np.cumsum(recv_sizes)]).astype(np.int64)
-        rows = b.mig_pack(off, n_loc)                      # (n_loc, 3): grouped by card-set owner
+        rows = b.mig_pack(off, n_loc)                      # (n_loc, 5) int32: grouped by card-set owner
         pieces = [rows[int(so[o]):int(so[o + 1])].reshape(-1) for o in range(W)]
-        rflat, hd = c.alltoall_pieces(pieces, recv_sizes * 3, what='parent rows')
+        rflat, hd = c.alltoall_pieces(pieces, recv_sizes * 5, what='parent rows')   # 20-byte rows: 5 int32
         c.wait(hd)
         n_exp = int(ro[-1])
         b.mig_expand(rflat, n_exp, st['n_parents'])
@@ -1156,7 +1156,7 @@ class HipBackend:
         return out
 
     def mig_pack(self, goff, n):
-        rows = torch.empty((max(int(n), 1), 3), dtype=torch.int64, device=self.device)
+        rows = torch.empty((max(int(n), 1), 5), dtype=torch.int32, device=self.device)
         self._chk(self.lib.sbd_mig_pack(self.h, int(goff), rows.data_ptr() if n else None), 'sbd_mig_pack')
         return rows[:int(n)]
 
