@@ -1151,7 +1151,8 @@ class HipBackend:
         self._chk(self.lib.sbd_mig_launch(self.h, int(self.world)), 'sbd_mig_launch')
 
     def mig_counts(self) -> np.ndarray:
-        out = np.zeros(self.world, np.int64)
+        """The slice's parents per card-set owner, then their raw children per owner (2 x world)."""
+        out = np.zeros(2 * self.world, np.int64)
         self._chk(self.lib.sbd_mig_counts(self.h, out.ctypes.data), 'sbd_mig_counts')
         return out
 
