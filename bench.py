@@ -298,7 +298,7 @@ def run_single(args):
 
 
 def rexpand_bytes(n_parents, n_raw, n_unique):
-    """Algorithmic bytes of k_rexpand per launch: the parent's 12-word state (96 B) and its
+    """Algorithmic bytes of k_rexpand2 per launch: the parent's 12-word state (96 B) and its
     24 B of candidate / lost masks; per raw child a 16 B visited-entry probe; per new key an 8 B tag CAS
     and an 8 B key store."""
     return 120 * n_parents + 16 * n_raw + 16 * n_unique
@@ -376,11 +376,11 @@ def run_realistic(args):
                       'segment_end': 'every stream', 'segments': segs,
                       'warmup_engine': 'own (the timed steps start on fresh engines)'},
            'phases_ms': ph,
-           'roofline': {'bound': 'hbm', 'kernel': 'k_rexpand', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+           'roofline': {'bound': 'hbm', 'kernel': 'k_rexpand2', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
                         'algorithmic_bytes_per_launch': int(byt), 'launch_ms': ph['ms_expand'], 'traffic': None},
            'cpu_baseline': None}
-    tr, tns, hit, src = pmc_traffic('k_rexpand<1>')
+    tr, tns, hit, src = pmc_traffic('k_rexpand2<1>')
     if tr is not None:
         out['roofline']['traffic'] = int(tr)
         out['roofline']['traffic_GBps'] = round(tr / (tns * 1e-9) / 1e9, 1)

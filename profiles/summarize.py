@@ -18,7 +18,7 @@ from collections import defaultdict
 # kernels launched once per step on the saturated path (k_expand: the last launches include the
 # pipelined expansion of the turn after the last timed one — one per step either way)
 PER_STEP = ['k_expand<false>', 'k_expand<true>', 'k_count_lm', 'k_count_lm_tiles', 'k_tk_stage', 'k_tk_unstage', 'k_scan_apply', 'k_emit_w<1, false>', 'k_tk_count', 'k_tk_write', 'k_os_hist', 'k_os_pass',
-            'k_gather_d', 'k_copy_idx', 'k_rexpand<1>', 'k_remit<1>', 'k_rgather']
+            'k_gather_d', 'k_copy_idx', 'k_rexpand<1>', 'k_rexpand2<1>', 'k_remit<1>', 'k_rgather']
 
 
 def short(name):
