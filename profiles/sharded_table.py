@@ -71,8 +71,10 @@ def overlap_flags(rows, others):
     return out
 
 
-def rank_table(rows, steps, ovl=None):
-    """ovl: per-row overlap flags; an overlapped kernel counts at the median of its clean instances."""
+def rank_table(rows, steps, ovl=None, cap=None):
+    """ovl: per-row overlap flags; an overlapped kernel counts at the median of its clean instances.  cap: per
+    kernel name, an upper bound on one instance's duration (the robust table: a launch that took longer than 1.5x
+    the median of its instances over all ranks waited on another process's work on the shared GPU)."""
     clean = defaultdict(list)
     if ovl is not None:
         for (name, t0, t1), o in zip(rows, ovl):
@@ -97,6 +99,8 @@ def rank_table(rows, steps, ovl=None):
             dt = (t1 - t0) / 1e6
             if o and name in med:
                 dt = med[name]
+            if cap is not None and name in cap:
+                dt = min(dt, cap[name])
             if name.startswith('k_apply_w'):
                 applied = True
             ph = None
@@ -144,17 +148,29 @@ def main():
         ranks.append(t)
         for k, v in u.items():
             unk[k] = max(unk.get(k, 0.0), v)
+    # robust table: every timed instance capped at 1.5x the median of its kernel's timed instances over all ranks
+    inst = defaultdict(list)
+    for rows in allrows:
+        cut = 'k_mig_digit' if any(r[0] == 'k_mig_digit' for r in rows) else 'k_raw_count'
+        ex = [i for i, r in enumerate(rows) if r[0] == cut]
+        for name, t0, t1 in rows[ex[-a.steps]:]:
+            inst[name].append((t1 - t0) / 1e6)
+    cap = {k: 1.5 * sorted(v)[len(v) // 2] for k, v in inst.items()}
+    robust = [rank_table(allrows[r], a.steps, None, cap)[0] for r in range(a.world)]
     keys = list(ranks[0].keys())
     mean = {k: sum(t[k] for t in ranks) / len(ranks) for k in keys}
     worst = {k: max(t[k] for t in ranks) for k in keys}
-    print(f'{"phase":34s} {"mean ms":>9s} {"max ms":>9s}')
+    rmean = {k: sum(t[k] for t in robust) / len(robust) for k in keys}
+    rworst = {k: max(t[k] for t in robust) for k in keys}
+    print(f'{"phase":34s} {"mean ms":>9s} {"max ms":>9s} {"robust":>9s} {"rob.max":>9s}')
     for k in keys:
-        print(f'{k:34s} {mean[k]:9.3f} {worst[k]:9.3f}')
+        print(f'{k:34s} {mean[k]:9.3f} {worst[k]:9.3f} {rmean[k]:9.3f} {rworst[k]:9.3f}')
     if unk:
         print('unclassified:', {k: round(v, 3) for k, v in unk.items()})
     if a.out:
         with open(a.out, 'w') as f:
             json.dump({'world': a.world, 'steps': a.steps, 'mean_ms': mean, 'max_ms': worst, 'per_rank_ms': ranks,
+                       'robust_mean_ms': rmean, 'robust_max_ms': rworst, 'robust_per_rank_ms': robust,
                        'unclassified_ms': unk}, f, indent=1)
 
 
