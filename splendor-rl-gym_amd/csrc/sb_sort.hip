@@ -686,11 +686,12 @@ __global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) { tk
 // always holds an earlier ticket, so it is resident and the wait ends.
 constexpr int OS_NT = 256;
 #ifndef SB_OS_IPT
-#define SB_OS_IPT 16
+#define SB_OS_IPT 8      // elements per thread: 8 x 1024 threads = 8192-element tiles (16 spills 45 VGPRs at 1024)
 #endif
 constexpr int OS_IPT = SB_OS_IPT;
 #ifndef SB_OS_PNT
-#define SB_OS_PNT 256    // threads per sort-pass workgroup (one tile of OS_PNT * OS_IPT elements)
+#define SB_OS_PNT 1024   // threads per sort-pass workgroup (one tile of OS_PNT * OS_IPT elements): with 10-bit
+                         // digits each thread owns one digit's look-back (OS_DPT = 1)
 #endif
 constexpr int OS_PNT = SB_OS_PNT;
 constexpr int OS_TILE = OS_PNT * OS_IPT;
@@ -703,9 +704,11 @@ constexpr int OS_LB = SB_OS_LB;
 #define SB_OS_DBG 0      // timing diagnostics only (wrong order): 1 no look-back, 2 unscattered writes
 #endif
 #ifndef SB_OS_D
-#define SB_OS_D 8        // digit bits per LSD pass.  10 (four passes for the 40-bit prefix instead of five) measured
-                         // 132 us per pass against 51 (1024-digit look-back per tile, 229 VGPRs: 2 waves per SIMD):
-                         // the sort 257 -> 527 us per step (profiles/r3/s5/ab_sort_digits.txt)
+#define SB_OS_D 10       // digit bits per LSD pass: four passes for the 40-bit prefix.  Round 4: 10-bit digits on
+                         // 1024-thread, 8192-element tiles (one digit per thread in the look-back, 107 VGPRs) against
+                         // round 3's 8-bit digits on 256 x 16: select 0.608-0.611 -> 0.583-0.584 ms on C3, 0.293 ->
+                         // 0.271-0.273 on C4 (profiles/r4/s2/sort_ab.txt).  Round 3 measured 10-bit digits on the
+                         // 256-thread tiles at 132 us per pass (four digits per thread, 229 VGPRs, 2 waves per SIMD)
 #endif
 constexpr int OS_D = SB_OS_D;
 constexpr int OS_B = 1 << OS_D;                     // bins per digit
