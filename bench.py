@@ -37,6 +37,8 @@ sys.path.insert(0, os.path.join(REPO, 'oracle'))
 METRIC = 'states expanded/sec per beam step, goal=15 beam_width=4M, 1/2/4/8 MI355X'
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 RANDOM_LOAD_PEAK_G = 48.0   # random 16-B loads / s over a 32 GiB table, measured (profiles/micro/r1_randaccess.txt)
+RANDOM_PROBE_G = 45.46    # random 16-B loads over a 32 GiB table (profiles/micro/fetchcal.hip, round 4)
+RANDOM_INSERT_G = 19.07   # probe + tag CAS + key store on one random line (same micro)
 GOAL = 15                   # C3 / C5 goal_pts
 # the reference's own CPU path on C3's heuristic, measured in the build container (BASELINE.md §2 / SURVEY §6):
 # pure Python, 1 core; it cannot run on the GPU box (the reference does not travel), so it is quoted, not timed
@@ -496,6 +498,16 @@ def main():
             'touches_per_launch': int(touches), 'achieved_G_per_s': round(touches / (ms_dom * 1e-3) / 1e9, 2),
             'peak_G_per_s': RANDOM_LOAD_PEAK_G, 'frac': round(touches / (ms_dom * 1e-3) / 1e9 / RANDOM_LOAD_PEAK_G, 3),
             'peak_source': 'profiles/micro/r1_randaccess.txt (load16, 32 GiB table)'}
+        # round 4: the same launch priced at the two rates calibrated with the counters on a 32 GiB table
+        # (profiles/micro/fetchcal.hip): a probe that settles with its load, and an insert (probe + tag CAS + key
+        # store on one line); displacing claims (atomicMin + lost mark) are left out, so this is a lower bound
+        new = uniq / len(per)
+        t_bound = ((raw / len(per) - new) / RANDOM_PROBE_G + new / RANDOM_INSERT_G) / 1e9 * 1e3
+        out['roofline']['random_access'].update({
+            'calibrated_bound_ms': round(t_bound, 3), 'frac_calibrated': round(t_bound / ms_dom, 3),
+            'calibrated_rates_G_per_s': {'probe': RANDOM_PROBE_G, 'insert': RANDOM_INSERT_G},
+            'calibration_source': 'profiles/r4/s2/fetchcal_plain.txt, fetchcal_pmc.txt (FETCH_SIZE x2 = 128 B per '
+                                  'random 16-B probe, the guide\'s gfx950 correction holds for random lines too)'})
     tr, tns, hit, src = pmc_traffic(dom.replace('ms_', 'k_'))
     if tr is not None:
         out['roofline']['traffic'] = int(tr)
