@@ -193,7 +193,8 @@ __device__ __forceinline__ void tk_pick_body(uint64_t* st) {
 }
 
 #ifndef SB_TK_CAND_PICK
-#define SB_TK_CAND_PICK 0   // candidate passes: SB_TK_CAND_GRID blocks, the last one picks (one launch per pass)
+#define SB_TK_CAND_PICK 0   // 1: candidate passes on SB_TK_CAND_GRID blocks, the last one picks (one launch per pass).
+                           // A/B (profiles/r4/s2/topk_cand_pick_ab.txt): slower on 64-512 blocks (select +20-220 us)
 #endif
 #ifndef SB_TK_CAND_GRID
 #define SB_TK_CAND_GRID 512
