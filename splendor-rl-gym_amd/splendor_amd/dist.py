@@ -193,6 +193,17 @@ class Comm:
         t = self._cp(lambda: torch.from_numpy(a).to(self.device))
         return self._gather_flat(t).cpu().numpy().reshape(self.world, len(a))
 
+    def allgather_var(self, arr: np.ndarray) -> np.ndarray:
+        """Every rank's int64 vector of any length, concatenated rank-major (host, gloo metadata group)."""
+        a = np.ascontiguousarray(arr, dtype=np.int64)
+        if self.world == 1:
+            return a
+        n = self.allgather_array(np.array([len(a)]), host=True)[:, 0]
+        pad = np.zeros(int(n.max()) if len(n) else 0, np.int64)
+        pad[:len(a)] = a
+        out = self.allgather_array(pad, host=True) if len(pad) else np.zeros((self.world, 0), np.int64)
+        return np.concatenate([out[r, :int(n[r])] for r in range(self.world)])
+
     def allgather_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """(world, *t.shape): every rank's equal-shape tensor, on this rank's device."""
         return self._back(self._gather_flat(t).reshape((self.world,) + tuple(t.shape)))
@@ -320,6 +331,9 @@ class DistSolve:
         self.counts = []                        # per turn: per-rank slice sizes
         # card-set ownership of the trail (HipBackend.MIG / sb_mig.inc): parents migrate to their card-set owners
         self.mig = bool(getattr(backend, 'mig', False)) and self.c.world > 1
+        # owner emission (with card-set ownership): survivors emitted on the expanding ranks, whose parents span
+        # every score level, so the kept records leave every rank evenly (HipBackend.OE / sb_oe.inc)
+        self.oe = self.mig and bool(getattr(backend, 'oe', False))
         self._launch_front(1)                   # runs while the host does the turn sync / goal check (the root)
         self.lookahead = True                   # step() launches the next turn's expansion before returning
         self._front_deferred = False            # lookahead was off: the next step() launches it
@@ -519,14 +533,46 @@ class DistSolve:
         sb = np.concatenate([[0], np.cumsum([nb(R[q][me]) for q in range(W)])]).astype(np.int64)
         rb = np.concatenate([[0], np.cumsum([nb(R[me][o]) for o in range(W)])]).astype(np.int64)
         bits = b.bits_buffer(int(sb[-1]))
-        b.mig_apply(back, bits, ro, sb[:-1])
+        b.mig_apply(back, bits, ro, sb[:-1], keep=self.oe)   # oe: the expand list's survivor masks kept for the emission
         rbits = b.bits_buffer(int(rb[-1]))
         c.alltoall_into([bits[int(sb[q]):int(sb[q + 1])] for q in range(W)],
                         [rbits[int(rb[o]):int(rb[o + 1])] for o in range(W)], what='survivor bits')
         all_n = c.gather_dev(b.mig_place(rbits, so, rb[:-1])).astype(np.int64)   # one wait for both
         b.apply_finish(int(all_n[c.rank]))
         self._mark(st, 'dedup_exchange')
+        if self.oe:
+            self._oe_emit(st, all_n, so, ro)
         return self._post_dedup(st, all_n, off)
+
+    def _oe_emit(self, st, all_n, so, ro):
+        """Owner emission: the range rank knows its parents' next_queue offsets (the survivor counts came back
+        with the bits) and holds the noise draws of its range; it sends each parent's global offset and its
+        survivors' draws to the rank that expanded the parent (rows' order), which emits them: scores, states,
+        global parent ranks and next_queue positions (the ties' order below)."""
+        c, b = self.c, self.b
+        me, W = c.rank, c.world
+        k_off, N = int(all_n[:me].sum()), int(all_n.sum())
+        self._oe_noise(N, all_n)
+        rgoff, rnoise, nb_send = b.oe_pack(k_off, N, so)             # row order; noise bytes per owner (host)
+        xnb = b.oe_counts(ro)                                         # expand side: survivors per source (host)
+        xgoff = b.u32_buffer(int(ro[-1]))
+        c.alltoall_into([rgoff[int(so[o]):int(so[o + 1])] for o in range(W)],
+                        [xgoff[int(ro[q]):int(ro[q + 1])] for q in range(W)], what='row offsets')
+        xnoise = None
+        if self.heur:
+            ns = np.concatenate([[0], np.cumsum(nb_send)]).astype(np.int64)
+            nr = np.concatenate([[0], np.cumsum(xnb)]).astype(np.int64)
+            xnoise = b.byte_buffer(int(nr[-1]))
+            c.alltoall_into([rnoise[int(ns[o]):int(ns[o + 1])] for o in range(W)],
+                            [xnoise[int(nr[q]):int(nr[q + 1])] for q in range(W)], what='noise draws')
+        b.oe_emit(xgoff, xnoise)
+        self._mark(st, 'oe_emit')
+
+    def _oe_noise(self, N, all_n):
+        if self.heur:
+            self.noise.prepare(self.consumed, N, all_n)
+            self.consumed += N
+        self._oe_noise_done = True
 
     def _dedup_parts(self, st, off):
         back = self._exchange_parts(st)
@@ -629,12 +675,15 @@ class DistSolve:
             self.done, self.winner = True, (self.turn, last)
             st.update(done=True, winner_rank=last)
             return st
-        if self.heur:
-            self.noise.prepare(self.consumed, N, all_n)
-            self.consumed += N
-        self._mark(st, 'noise')
-        b.emit(k_off, N, off)
-        self._mark(st, 'emit')
+        oe = getattr(self, '_oe_noise_done', False)
+        self._oe_noise_done = False
+        if not oe:   # (owner emission: the range ranks' draws went out with the offsets, _oe_emit)
+            if self.heur:
+                self.noise.prepare(self.consumed, N, all_n)
+                self.consumed += N
+            self._mark(st, 'noise')
+            b.emit(k_off, N, off)
+            self._mark(st, 'emit')
         K = min(N, self.W) if self.heur else N
         G = c.world
         if self.heur:
@@ -644,14 +693,23 @@ class DistSolve:
             if pos:
                 self._multiselect(pos, st)
                 self._mark(st, 'sel_passes')
-                if has_top:
+                if has_top and oe:   # ties at the keep boundary in next_queue order: by position, over all ranks
+                    tp, need = b.oe_ties()
+                    allt = c.allgather_var(tp)
+                    pstar = int(np.partition(allt, need - 1)[need - 1]) if need > 0 else -1
+                elif has_top:
                     eq_all = c.allgather_tensor(b.sel_eq()).reshape(-1)
             self._mark(st, 'sel_eq')
-            dest_dev = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
+            if oe:
+                dest_dev = b.oe_partition(has_top, pstar if has_top else -1, len(pos) - int(has_top), G)
+            else:
+                dest_dev = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
+        elif oe:
+            dest_dev = b.oe_partition_bfs(N, G)
         else:
             dest_dev = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
-        rec = b.pack_kept(all_n[c.rank])   # enqueued ahead of the counts' round trip
+        rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank])   # enqueued ahead of the counts' round trip
         if c.world == 1:   # every kept record stays: K of them, known here (no round trip)
             dest_counts = recv = np.array([K], dtype=np.int64)
         else:

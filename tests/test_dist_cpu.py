@@ -49,6 +49,7 @@ def _worker(rank, world, port, cfg, outdir):
     b.parts = cfg.get('parts', 0)   # > 0: the pipelined protocol (the HIP key pass's exchange parts)
     if cfg.get('mig'):   # card-set ownership of the trail (sb_mig.inc restated); 'force0': every card set to rank 0
         b.mig, b.force0 = True, cfg.get('force0', False)
+        b.oe = cfg.get('oe', False)   # owner emission: survivors emitted on the expanding ranks
         b.parts = b.parts or 2
     if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
         from deferred_comm import DeferredComm
@@ -125,6 +126,20 @@ CASES = [
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'mig': True}),
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'mig': True}),
     (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'mig': True, 'force0': True}),
+    # owner emission: the survivors emitted on the expanding ranks (offsets and noise draws sent there), ties at the
+    # keep boundary by next_queue position over all ranks, the receiver orders by (score, position)
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'mig': True, 'oe': True}),
+    (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True, 'mig': True, 'oe': True,
+         'parts': 3}),
+    (4, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'mig': True, 'oe': True,
+         'deferred': True}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'mig': True, 'oe': True,
+         'parts': 1}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'mig': True, 'oe': True}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'mig': True,
+         'oe': True}),
+    (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'mig': True, 'force0': True,
+         'oe': True}),
 ]
 
 
