@@ -67,7 +67,8 @@ typedef struct {
                                   the host when it expands with sbd_expand_parts); bit 7 (test): the key
                                   pass gives every key (with bit 8: every card set) to rank 0 (parts that
                                   send no records; results unchanged); bit 8: card-set ownership of the
-                                  sharded trail (sbd_mig_*, world_size > 1) */
+                                  sharded trail (sbd_mig_*, world_size > 1); bit 9 (with bit 8): owner
+                                  emission (sbd_oe_*) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -337,6 +338,26 @@ int sbd_mig_apply(sb_engine* e, const uint8_t* d_back, uint8_t* d_bits, int32_t 
                   const int64_t* seg_byte);
 int sbd_mig_place(sb_engine* e, const uint8_t* d_bits, int32_t nown, const int64_t* group_start,
                   const int64_t* byte_base, void* n_unique_dev);
+/* ---- owner emission (flags bit 9 with bit 8; csrc/sb_oe.inc): the survivors are emitted on the expanding
+ * (card-set owner) ranks, whose parents span every score level, so the kept records leave every rank evenly.
+ *   range side:  after sbd_mig_place / sbd_apply_finish, sbd_oe_pack (each row's global next_queue offset and
+ *                its survivors' noise draws, rows' order; the noise bytes per owner on the host — waits; consumes
+ *                the turn's draws), all_to_all of both by the caller
+ *   expand side: sbd_mig_apply keeps the expand list's masks; sbd_oe_counts (survivors per source segment, host —
+ *                waits), sbd_oe_emit (the emission over the expand list: states, keys, global parent ranks,
+ *                next_queue positions), then the joint select as usual; at the keep boundary sbd_oe_ties +
+ *                sbd_oe_tie_read (this rank's tie positions; the caller gathers every rank's and takes the
+ *                need-th smallest, pstar), sbd_oe_partition (kept: key > T or key == T and position <= pstar) or
+ *                sbd_oe_partition_bfs, sbd_pack_kept (the par word carries the position << 32)
+ *   receive:     sbd_receive orders the records by (score desc, position asc) */
+int sbd_oe_pack(sb_engine* e, uint64_t k_off, uint64_t n_total, uint32_t* d_rgoff, uint8_t* d_rnoise, int32_t nown,
+                const int64_t* group_start, int64_t* nb_out);
+int sbd_oe_counts(sb_engine* e, int32_t nseg, const int64_t* seg_start, int64_t* out);
+int sbd_oe_emit(sb_engine* e, const uint32_t* d_xgoff, const uint8_t* d_xnoise);
+int sbd_oe_ties(sb_engine* e, int64_t* count, int64_t* need);
+int sbd_oe_tie_read(sb_engine* e, int64_t* pos, int64_t count);
+int sbd_oe_partition(sb_engine* e, int32_t has_top, int64_t pstar, int32_t nsplit, int32_t world, void* dest_counts_dev);
+int sbd_oe_partition_bfs(sb_engine* e, uint64_t n_total, int32_t world, void* dest_counts_dev);
 /* flags bit 0: device time (ms) of the last pipelined expansion's key kernels (k_keys_a / k_mkeys_a, summed
  * over its parts; waits for them) — the bench's roofline of the dominant world > 1 kernel */
 int sbd_keypass_ms(sb_engine* e, float* ms);

@@ -898,6 +898,13 @@ struct Engine {
     DBuf<uint64_t> xlo, xhi, mtag;
     uint32_t* h_mpc = nullptr;
     hipEvent_t mig_ev = nullptr;
+    // owner emission (sb_oe.inc, cfg flags bit 9 with bit 8): the expand list's survivor masks and offsets, the
+    // emitted survivors' next_queue positions, the keep boundary's tie positions, the second receive order
+    bool oe = false;
+    int64_t oe_n = 0;                     // survivors emitted on this rank (the expand list's)
+    DBuf<unsigned long long> xsurv;
+    DBuf<uint32_t> xsoff, kpos, tpos, rowcnt, rownb, kidx2, oe_small;
+    uint32_t* h_oe = nullptr;             // pinned: per-group totals, tie count
     // sharded key pass timing (flags bit 0): an event pair around each part's key kernel (k_keys_a / k_mkeys_a)
     hipEvent_t kp_ev[32] = {};
     int kp_n = 0;
@@ -1474,6 +1481,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
                 throw HipError{hipErrorInvalidValue, "bad rank / world_size (<= 64)"};
             E.own_mask = cap - 1;
             E.mig = (cfg->flags & 256) != 0 && cfg->world_size > 1;   // card-set ownership (sb_mig.inc)
+            E.oe = E.mig && (cfg->flags & 512) != 0;                    // owner emission (sb_oe.inc)
             SB_HIP(hipMalloc((void**)&E.own, cap * sizeof(Entry)));
             SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
         }
@@ -1784,6 +1792,15 @@ void sb_destroy(sb_engine* h) {
     E.mrawsend.release();
     E.mrawoff.release();
     E.mrawown.release();
+    E.xsurv.release();
+    E.xsoff.release();
+    E.kpos.release();
+    E.tpos.release();
+    E.rowcnt.release();
+    E.rownb.release();
+    E.kidx2.release();
+    E.oe_small.release();
+    if (E.h_oe) (void)hipHostFree(E.h_oe);
     if (E.h_mpc) (void)hipHostFree(E.h_mpc);
     if (E.mig_ev) (void)hipEventDestroy(E.mig_ev);
     for (auto& e : E.kp_ev)

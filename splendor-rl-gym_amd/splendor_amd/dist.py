@@ -553,7 +553,7 @@ class DistSolve:
         me, W = c.rank, c.world
         k_off, N = int(all_n[:me].sum()), int(all_n.sum())
         self._oe_noise(N, all_n)
-        rgoff, rnoise, nb_send = b.oe_pack(k_off, N, so)             # row order; noise bytes per owner (host)
+        rgoff, rnoise, nb_send = b.oe_pack(k_off, N, so, int(all_n[me]))   # rows' order; noise bytes per owner
         xnb = b.oe_counts(ro)                                         # expand side: survivors per source (host)
         xgoff = b.u32_buffer(int(ro[-1]))
         c.alltoall_into([rgoff[int(so[o]):int(so[o + 1])] for o in range(W)],
@@ -866,6 +866,8 @@ class HipBackend:
     KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'
     # world > 1: card-set ownership of the trail (flags bit 8, sb_mig.inc) instead of key ownership
     MIG = os.environ.get('SB_DIST_MIG', '0') == '1'
+    # with card-set ownership: owner emission (flags bit 9, sb_oe.inc), survivors emitted on the expanding ranks
+    OE = os.environ.get('SB_DIST_OE', '0') == '1'
     PARTS = int(os.environ.get('SB_DIST_PARTS', '4'))   # exchange parts of the pipelined key pass (<= 16)
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
@@ -880,11 +882,13 @@ class HipBackend:
         self.device = torch.device('cuda', device_index)
         torch.cuda.set_device(self.device)
         self.mig = bool(self.MIG or (int(extra_flags) & 256)) and world > 1
+        self.oe = self.mig and bool(self.OE or (int(extra_flags) & 512))
         self.timing = bool(int(extra_flags) & 1)   # key-pass device time per step (sbd_keypass_ms)
+        self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
                          flags=2 | (int(extra_flags) & 177) | (64 if self.KEYPASS and world > 1 else 0) |
-                         (256 if self.mig else 0),
+                         (256 if self.mig else 0) | (512 if self.oe else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
@@ -954,6 +958,13 @@ class HipBackend:
         lib.sbd_mig_apply.argtypes = [vp, vp, vp, i32, vp, vp]
         lib.sbd_mig_place.argtypes = [vp, vp, i32, vp, vp, vp]
         lib.sbd_keypass_ms.argtypes = [vp, vp]
+        lib.sbd_oe_pack.argtypes = [vp, u64, u64, vp, vp, i32, vp, vp]
+        lib.sbd_oe_counts.argtypes = [vp, i32, vp, vp]
+        lib.sbd_oe_emit.argtypes = [vp, vp, vp]
+        lib.sbd_oe_ties.argtypes = [vp, vp, vp]
+        lib.sbd_oe_tie_read.argtypes = [vp, vp, i64]
+        lib.sbd_oe_partition.argtypes = [vp, i32, i64, i32, i32, vp]
+        lib.sbd_oe_partition_bfs.argtypes = [vp, u64, i32, vp]
         lib._sbd_bound = True
 
     def _chk(self, rc, what):
@@ -1235,7 +1246,7 @@ class HipBackend:
         last bit); the caller slices [0, nbytes)."""
         return torch.zeros(((int(nbytes) + 7) // 8 + 2) * 8, dtype=torch.uint8, device=self.device)
 
-    def mig_apply(self, back, bits, seg_start, seg_byte):
+    def mig_apply(self, back, bits, seg_start, seg_byte, keep=False):   # keep: implied by the engine's flags bit 9
         st = np.ascontiguousarray(seg_start, dtype=np.int64)
         sb = np.ascontiguousarray(seg_byte, dtype=np.int64)
         self._chk(self.lib.sbd_mig_apply(self.h, back.data_ptr() if back.numel() else None, bits.data_ptr(),
@@ -1248,6 +1259,63 @@ class HipBackend:
         self._chk(self.lib.sbd_mig_place(self.h, rbits.data_ptr(), len(bb), gs.ctypes.data, bb.ctypes.data,
                                          n.data_ptr()), 'sbd_mig_place')
         return n
+
+    # ---------------------------------------------------------------- owner emission (sb_oe.inc)
+    def oe_pack(self, k_off, N, so, n_unique_local):
+        """Range side: rows' global offsets (u32) and their survivors' noise draws (bytes), rows' order; the noise
+        bytes per owner on the host (waits for them)."""
+        n = self.n_local()
+        rgoff = self._empty(max(n, 1), torch.int32)[:n]
+        heur = getattr(self, 'heur', True)
+        rnoise = self._empty(max(int(n_unique_local), 1), torch.uint8)[:int(n_unique_local)]
+        gs = np.ascontiguousarray(so, dtype=np.int64)
+        nb = np.zeros(len(gs) - 1, np.int64)
+        self._chk(self.lib.sbd_oe_pack(self.h, int(k_off), int(N), rgoff.data_ptr() if n else None,
+                                       rnoise.data_ptr() if heur else None, len(gs) - 1, gs.ctypes.data, nb.ctypes.data),
+                  'sbd_oe_pack')
+        return rgoff, rnoise, nb
+
+    def oe_counts(self, ro):
+        """Expand side: survivors per source segment (host; waits), their offsets on the device."""
+        gs = np.ascontiguousarray(ro, dtype=np.int64)
+        out = np.zeros(len(gs) - 1, np.int64)
+        self._chk(self.lib.sbd_oe_counts(self.h, len(gs) - 1, gs.ctypes.data, out.ctypes.data), 'sbd_oe_counts')
+        self._oe_n = int(out.sum())
+        return out
+
+    def u32_buffer(self, n):
+        return self._empty(max(int(n), 1), torch.int32)[:int(n)]
+
+    def byte_buffer(self, n):
+        return self._empty(max(int(n), 1), torch.uint8)[:int(n)]
+
+    def oe_emit(self, xgoff, xnoise):
+        self._chk(self.lib.sbd_oe_emit(self.h, xgoff.data_ptr() if xgoff.numel() else None,
+                                       xnoise.data_ptr() if xnoise is not None and xnoise.numel() else None),
+                  'sbd_oe_emit')
+
+    def oe_n(self):
+        return self._oe_n
+
+    def oe_ties(self):
+        C = self.C
+        cnt, need = C.c_int64(), C.c_int64()
+        self._chk(self.lib.sbd_oe_ties(self.h, C.byref(cnt), C.byref(need)), 'sbd_oe_ties')
+        pos = np.zeros(cnt.value, np.int64)
+        if cnt.value:
+            self._chk(self.lib.sbd_oe_tie_read(self.h, pos.ctypes.data, cnt.value), 'sbd_oe_tie_read')
+        return pos, need.value
+
+    def oe_partition(self, has_top, pstar, nsplit, G):
+        counts = torch.zeros(G, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_oe_partition(self.h, int(bool(has_top)), int(pstar), int(nsplit), int(G), counts.data_ptr()),
+                  'sbd_oe_partition')
+        return counts
+
+    def oe_partition_bfs(self, N, G):
+        counts = torch.zeros(G, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_oe_partition_bfs(self.h, int(N), int(G), counts.data_ptr()), 'sbd_oe_partition_bfs')
+        return counts
 
     def receive(self, rec, heur):
         self._chk(self.lib.sbd_receive(self.h, rec.data_ptr() if rec.numel() else None, rec.shape[0], int(bool(heur))),

@@ -51,6 +51,20 @@ def test_realistic_c4_w1m_oracle_golden():
     eng.close()
 
 
+def _wait_device_memory(min_free_gib=240.0, timeout_s=120.0):
+    """Wait until the device has released a previous multi-process test's memory (eight ranks of C5 need most
+    of the 288 GB; the exited ranks' allocations are reclaimed asynchronously)."""
+    import time
+
+    import torch
+    t0 = time.time()
+    while time.time() - t0 < timeout_s:
+        free, _ = torch.cuda.mem_get_info(0)
+        if free >= min_free_gib * 2**30:
+            return
+        time.sleep(2.0)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
@@ -181,7 +195,7 @@ def test_c5_w32m_single_gpu_oracle_golden():
 
 
 @pytest.mark.skipif(not golden_exists(C5), reason='C5 golden not generated')
-@pytest.mark.parametrize('mig', [False, True])
+@pytest.mark.parametrize('mig', [False, True, 'oe'])
 def test_c5_sharded_world8_oracle_golden(mig):
     """C5 as the 8-GPU job runs it, 8 ranks on one GPU (gloo transport, HIP per-rank primitives, 4M
     states per rank): every turn's digest over the rank slices, sizes, path, final MT state on every
@@ -191,7 +205,9 @@ def test_c5_sharded_world8_oracle_golden(mig):
     world = 8
     cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
            'visited_log2': 28, 'digest_inline': True,
-           'flags': 32 | (256 if mig else 0)}   # 8 ranks share one GPU's HBM; 256: card-set ownership
+           'flags': 32 | (256 if mig else 0) | (512 if mig == 'oe' else 0)}   # 8 ranks share one GPU's HBM; 256:
+    # card-set ownership; 512: owner emission
+    _wait_device_memory()
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]

@@ -104,6 +104,15 @@ CASES = [
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10, 'flags': 256}),
     # every card set owned by rank 0: the other ranks expand nothing, rank 0 sends no records
     (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 384}),
+    # owner emission (flags bit 9, sb_oe.inc): survivors emitted on the expanding ranks with the offsets and draws
+    # the range ranks send; keep-boundary ties by position over all ranks; receivers order by (score, position)
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'flags': 768}),
+    (3, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 768}),
+    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'flags': 768}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'flags': 768}),
+    (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1, 'flags': 768,
+         'parts': 1}),
+    (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 896}),
 ]
 
 
