@@ -24,10 +24,10 @@ PHASES = [
     ('answer bits', r'^k_(un)?pack_bits'),
     ('apply', r'^k_apply_w|^k_count_masks|^k_counts_i64|^k_total_i64'),
     ('noise (side stream)', r'^k_mt_'),
-    ('emit', r'^k_emit_w'),
-    ('joint select', r'^k_ds_|^k_tk_'),
+    ('emit', r'^k_emit_w|^k_oe_(rowcnt|groups|pack|fix)'),
+    ('joint select', r'^k_ds_|^k_tk_|^k_oe_ties'),
     ('rebalance partition', r'^k_dest|^k_part_'),
-    ('receive sort + gather', r'^k_recv_|^k_iota|^k_os_|^k_fx_|^k_copy_idx'),
+    ('receive sort + gather', r'^k_recv_|^k_iota|^k_os_|^k_fx_|^k_copy_idx|^k_oe_recv|^k_oe_compose'),
 ]
 
 
