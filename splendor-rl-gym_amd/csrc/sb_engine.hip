@@ -800,6 +800,12 @@ static unsigned grid_cap(int64_t work, int per_block, unsigned cap) {
     return (unsigned)std::min<int64_t>(g, cap);
 }
 
+// owner emission (sb_oe.inc): row group starts (card-set owners) / received source segments, start[ng] = n
+struct OeGroups {
+    uint32_t start[65];
+    int ng;
+};
+
 struct Engine {
     sb_config cfg{};
     int dev = 0;
@@ -903,7 +909,8 @@ struct Engine {
     bool oe = false;
     int64_t oe_n = 0;                     // survivors emitted on this rank (the expand list's)
     DBuf<unsigned long long> xsurv;
-    DBuf<uint32_t> xsoff, kpos, tpos, rowcnt, rownb, kidx2, oe_small;
+    DBuf<uint32_t> xsoff, kpos, tpos, rowcnt, rownb, kidx2, rpos, oe_small;
+    OeGroups oe_rg{};   // owner emission: the next sbd_receive's source segments (sbd_oe_segments)
     uint32_t* h_oe = nullptr;             // pinned: per-group totals, tie count
     // sharded key pass timing (flags bit 0): an event pair around each part's key kernel (k_keys_a / k_mkeys_a)
     hipEvent_t kp_ev[32] = {};
@@ -1799,6 +1806,7 @@ void sb_destroy(sb_engine* h) {
     E.rowcnt.release();
     E.rownb.release();
     E.kidx2.release();
+    E.rpos.release();
     E.oe_small.release();
     if (E.h_oe) (void)hipHostFree(E.h_oe);
     if (E.h_mpc) (void)hipHostFree(E.h_mpc);

@@ -38,7 +38,7 @@ EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_read_next', 'sb_prune'
             'sbd_key_range', 'sbd_sel_begin', 'sbd_sel_hist', 'sbd_sel_pick', 'sbd_sel_compact', 'sbd_sel_eq', 'sbd_set_stream', 'sbd_noise_info', 'sbd_noise_chunk', 'sbd_noise_sync', 'sbd_noise_pack', 'sbd_noise_fill', 'sbd_partition', 'sbd_partition_bfs', 'sbd_pack_kept', 'sbd_receive', 'sbd_mark_done',
             'sbd_mig_launch', 'sbd_mig_counts', 'sbd_mig_pack', 'sbd_mig_expand', 'sbd_mig_claim', 'sbd_mig_apply', 'sbd_mig_place', 'sbd_keypass_ms',
             'sbd_oe_pack', 'sbd_oe_counts', 'sbd_oe_emit', 'sbd_oe_ties', 'sbd_oe_tie_read', 'sbd_oe_partition',
-            'sbd_oe_partition_bfs',
+            'sbd_oe_partition_bfs', 'sbd_oe_segments',
             'sbr_create', 'sbr_step', 'sbr_read_turn', 'sbr_path')
 
 

@@ -726,7 +726,10 @@ class DistSolve:
             rrec[int(ro[me]):int(ro[me + 1])].copy_(rec[int(so[me]):int(so[me + 1])])
         else:
             rrec = rec[:int(dest_counts.sum())]
+            ro = np.array([0, rrec.shape[0]], dtype=np.int64)
         self._mark(st, 'a2a_kept')
+        if oe:   # each source's records in position order: the receive merges them
+            b.oe_segments(ro)
         b.receive(rrec, self.heur)
         if self.heur:
             self.noise.background()
@@ -965,6 +968,7 @@ class HipBackend:
         lib.sbd_oe_tie_read.argtypes = [vp, vp, i64]
         lib.sbd_oe_partition.argtypes = [vp, i32, i64, i32, i32, vp]
         lib.sbd_oe_partition_bfs.argtypes = [vp, u64, i32, vp]
+        lib.sbd_oe_segments.argtypes = [vp, i32, vp]
         lib._sbd_bound = True
 
     def _chk(self, rc, what):
@@ -1316,6 +1320,10 @@ class HipBackend:
         counts = torch.zeros(G, dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_oe_partition_bfs(self.h, int(N), int(G), counts.data_ptr()), 'sbd_oe_partition_bfs')
         return counts
+
+    def oe_segments(self, seg_start):
+        gs = np.ascontiguousarray(seg_start, dtype=np.int64)
+        self._chk(self.lib.sbd_oe_segments(self.h, len(gs) - 1, gs.ctypes.data), 'sbd_oe_segments')
 
     def receive(self, rec, heur):
         self._chk(self.lib.sbd_receive(self.h, rec.data_ptr() if rec.numel() else None, rec.shape[0], int(bool(heur))),
