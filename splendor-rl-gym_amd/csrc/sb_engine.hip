@@ -865,6 +865,8 @@ struct Engine {
     DBuf<uint64_t> rkey;                  // sharded receive: keys of the received records
     DBuf<uint8_t> digit;
     DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
+    DBuf<uint16_t> mrj;                   // card-set records: (parent in chunk << 8) | move, at the record's slot
+    DBuf<uint32_t> mcrec;                 // card-set records per 64-parent chunk of the expand list
     // visited-set growth (grow_table): largest raw children per parent seen so far, tables rebuilt
     double raw_ratio = 32.0;
     int n_grow = 0;
@@ -1779,6 +1781,8 @@ void sb_destroy(sb_engine* h) {
     E.part_hist.release();
     E.digit.release();
     E.rdsc.release();
+    E.mrj.release();
+    E.mcrec.release();
     if (E.s_claim) (void)hipStreamSynchronize(E.s_claim);
     E.ks_rdr.release();
     E.ks_sown.release();
