@@ -129,6 +129,15 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
                          hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false,
                          const uint32_t* payload = nullptr, bool full_key = false);
 // fill_ff (optional): 256 u32 words set to ~0 by the same launch (the gather's per-pts first-rank table)
+// fused first select pass (the producer's histogram): bins of key >> SB_SEL_FSH over a 2048-bin window.  47 (default):
+// 1/32-binade bins below the previous maximum, then a second pass over all keys before the partition.  42 (A/B,
+// rejected): 1/1024-binade bins around the previous threshold and no second pass — but C3's scores are so
+// discrete (≈115k distinct values in the kept 4M) that the threshold's bin still holds millions of keys, and
+// copying them as candidates costs more than the pass it saves (select 0.578 -> 0.578-0.588 ms; stage 89 -> 130-143
+// us, unstage 30 -> 47-76 us: profiles/r4/s2/fsh_ab.txt)
+#ifndef SB_SEL_FSH
+#define SB_SEL_FSH 47
+#endif
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false,
                                      uint32_t* fill_ff = nullptr);
 unsigned long long* topk_fused_hist(TopkScratch& s);

@@ -72,7 +72,7 @@ enum : int {
     ST_BASE2,   // output offset of group 2 (= A)
     ST_BASE3,   // output offset of group 3 (= A + G2)
     ST_TOPK,    // sort: bits [0, TOPK) vary among the kept keys
-    ST_FBASE,   // fused first pass: histogram bin b counts keys with key >> 47 == FBASE + b (edges clamped)
+    ST_FBASE,   // fused first pass: histogram bin b counts keys with key >> SB_SEL_FSH == FBASE + b (edges clamped)
     ST_FALLBACK,  // fused first pass unusable (threshold in a clamped bin): run the generic first pass
     ST_SLO,     // sort: lowest possible kept key; digits are taken from (key - SLO) >> SH32
     ST_SH32,    // sort: low bits below the sorted 40-bit prefix
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(TK_NT) void k_tk_pick(uint64_t* st, int only_fallba
     tk_pick_body<TK_NT, false>(st);
 }
 
-// First pass from the histogram the emission folded (bins of key >> 47 in [FBASE, FBASE + 2048), the
+// First pass from the histogram the emission folded (bins of key >> SB_SEL_FSH in [FBASE, FBASE + 2048), the
 // edge bins clamped): pick the bin holding the keep-th largest key.  An edge bin mixes prefixes, so a
 // threshold there (or a count that is not n) sets FALLBACK and the generic first pass runs instead.
 __device__ __forceinline__ void tk_pick_fused_body(uint64_t* st, int64_t n) {
@@ -337,7 +337,7 @@ __device__ __forceinline__ void tk_pick_fused_body(uint64_t* st, int64_t n) {
             const uint64_t nneed = need - cum;
             st[ST_NEED] = nneed;
             st[ST_PREFIX] = st[ST_FBASE] + (uint64_t)b;
-            st[ST_SH] = 47;
+            st[ST_SH] = SB_SEL_FSH;
             st[ST_DONE] = c[j] == nneed;
             st[ST_FALLBACK] = 0;
         }
@@ -698,7 +698,8 @@ constexpr int OS_PNT = SB_OS_PNT;
 constexpr int OS_TILE = OS_PNT * OS_IPT;
 constexpr int OS_NW = OS_PNT / 64;   // waves per pass workgroup
 #ifndef SB_OS_LB
-#define SB_OS_LB 8       // predecessors polled together per look-back round
+#define SB_OS_LB 8       // predecessors polled together per look-back round (16: 123 VGPRs, select +20-30 us on C3,
+                         // +10 on C4; 32 spills: profiles/r4/s2/fsh_ab.txt)
 #endif
 constexpr int OS_LB = SB_OS_LB;
 #ifndef SB_OS_DBG
@@ -1209,8 +1210,14 @@ __global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window, uint32
     if (fill_ff) fill_ff[threadIdx.x] = 0xFFFFFFFFu;   // the caller's 256-word table (the gather's first ranks)
     if (threadIdx.x == 0) {
         if (fused) {
-            const int64_t top = (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
-            st[ST_FBASE] = off_window ? 0 : (top < 0 ? 0 : (uint64_t)top);
+            int64_t b0;
+            if (SB_SEL_FSH == 47) {   // round 3: the top bin two binades above the previous maximum
+                b0 = (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
+            } else {   // half a binade below the previous threshold (ST_SLO: the lowest kept key) to 1.5 above
+                const uint64_t ref = st[ST_SLO] ? st[ST_SLO] : st[ST_MAX];
+                b0 = (int64_t)(ref >> SB_SEL_FSH) - (int64_t)((1ull << 52) >> SB_SEL_FSH) / 2;
+            }
+            st[ST_FBASE] = off_window ? 0 : (b0 < 0 ? 0 : (uint64_t)b0);
         }
         st[ST_MIN] = ~0ull;
         st[ST_MAX] = 0;
@@ -1302,8 +1309,9 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         tk_hist_pick(s, st, keys, n, nullptr, stv, (int)fused, hg);
         // more digits over all keys before the partition: the scores crowd into few first-pass bins (about
         // half of C3's keys share the threshold's), so the partition would copy most keys as candidates
+        // (with the fine fused bins, SB_SEL_FSH < 47, only after a fallback to the generic first pass)
         for (int e = 0; e < SEL_PREPASS; e++) {
-            tk_hist_pick(s, st, keys, n, nullptr, stv, 0, hg);
+            tk_hist_pick(s, st, keys, n, nullptr, stv, (fused && SB_SEL_FSH < 47) ? 1 : 0, hg);
         }
         const unsigned cg = (unsigned)std::min<int64_t>(ntiles, TK_COUNT_GRID);
         const unsigned wg = (unsigned)std::min<int64_t>(ntiles, TK_WRITE_GRID);
