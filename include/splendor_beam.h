@@ -361,6 +361,9 @@ int sbd_oe_partition_bfs(sb_engine* e, uint64_t n_total, int32_t world, void* de
 /* receive side: the next sbd_receive's records arrive as nseg source segments (seg_start[0..nseg], each segment in
  * next_queue position order); sbd_receive merges them by position, then orders them stably by score */
 int sbd_oe_segments(sb_engine* e, int32_t nseg, const int64_t* seg_start);
+/* test hook: the receive merge alone (host positions, nseg ascending segments; out_idx[rank] = record) */
+int sb_debug_oe_merge(int32_t device, const uint32_t* pos, int64_t m, int32_t nseg, const int64_t* seg_start,
+                      uint32_t* out_idx);
 /* flags bit 0: device time (ms) of the last pipelined expansion's key kernels (k_keys_a / k_mkeys_a, summed
  * over its parts; waits for them) — the bench's roofline of the dominant world > 1 kernel */
 int sbd_keypass_ms(sb_engine* e, float* ms);

@@ -109,6 +109,33 @@ def test_device_topk_stable():
         assert np.array_equal(got, exp.astype(np.uint32)), (n, keep, distinct)
 
 
+def test_device_oe_merge_segments():
+    """The owner-emission receive merge (sb_oe.inc k_oe_merge) against a sort of the positions: segments of
+    ascending, distinct positions, evenly interleaved, a sparse segment beside dense ones (the per-lane
+    fallback past OE_MERGE_SPAN), empty segments, a single segment, 64 segments, runs of 64 and off-by-one sizes."""
+    import ctypes as C
+    from splendor_amd import _lib
+    rng = np.random.default_rng(11)
+
+    def case(sizes, spread):
+        m = int(sum(sizes))
+        pos = rng.choice(spread, m, replace=False).astype(np.uint32)
+        owner = rng.permutation(np.repeat(np.arange(len(sizes)), sizes))   # which segment each position joins
+        segs = [np.sort(pos[owner == q]) for q in range(len(sizes))]
+        flat = np.ascontiguousarray(np.concatenate(segs).astype(np.uint32))
+        start = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        out = np.empty(m, np.uint32)
+        _lib.check(_lib.lib().sb_debug_oe_merge(0, flat, m, len(sizes), start, out), 'sb_debug_oe_merge')
+        assert np.array_equal(out, np.argsort(flat, kind='stable').astype(np.uint32)), sizes[:8]
+
+    case([100_000], 10**6)
+    case([50_000] * 8, 2**31)
+    case([1, 2, 63, 64, 65, 127, 128, 129], 10**4)
+    case([300_000, 17, 300_000, 0, 5, 200_000, 3, 0], 2**32 - 1)   # sparse segments among dense ones
+    case([0, 0, 4096, 0], 10**5)
+    case(list(rng.integers(0, 3000, 64)), 10**7)
+
+
 def test_device_topk_key_ranges():
     """Select/sort over u64 keys spanning the full range, all-equal keys, keys differing only in low
     bits, keep > n, and a threshold inside a heavily tied bucket (stable descending order)."""
