@@ -139,7 +139,7 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #define SB_SEL_FSH 47
 #endif
 unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused = false, bool off_window = false,
-                                     uint32_t* fill_ff = nullptr);
+                                     uint32_t* fill_ff = nullptr, int fill_n = 256);
 unsigned long long* topk_fused_hist(TopkScratch& s);
 const uint64_t* topk_fused_base(TopkScratch& s);
 // size the scratch for n keys and keep kept (avoids allocation on the step path)

@@ -1206,8 +1206,9 @@ void TopkScratch::release() {
 // before the producer of a turn's keys runs: reset the key range; with fused = 1 also place the fused
 // first-pass window (from the previous turn's maximum: its top bin sits 64 bins (two binades) above
 // it) and zero the histogram the producer adds to
-__global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window, uint32_t* fill_ff) {
-    if (fill_ff) fill_ff[threadIdx.x] = 0xFFFFFFFFu;   // the caller's 256-word table (the gather's first ranks)
+__global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window, uint32_t* fill_ff, int fill_n) {
+    if (fill_ff)   // the caller's fill_n-word table (the gather's first ranks)
+        for (int i = threadIdx.x; i < fill_n; i += blockDim.x) fill_ff[i] = 0xFFFFFFFFu;
     if (threadIdx.x == 0) {
         if (fused) {
             int64_t b0;
@@ -1252,9 +1253,10 @@ void topk_reserve(TopkScratch& s, int64_t n, int64_t keep) {
     }
 }
 
-unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window, uint32_t* fill_ff) {
+unsigned long long* topk_range_reset(TopkScratch& s, hipStream_t st, bool fused, bool off_window, uint32_t* fill_ff,
+                                     int fill_n) {
     s.small.ensure(ST_WORDS);
-    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(256), 0, st, s.small.p, (int)fused, (int)off_window, fill_ff);
+    hipLaunchKernelGGL(k_tk_range_reset, dim3(1), dim3(256), 0, st, s.small.p, (int)fused, (int)off_window, fill_ff, fill_n);
     return (unsigned long long*)(s.small.p + ST_MIN);
 }
 
