@@ -416,15 +416,28 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
                                                    int slot_eq, int phase2, uint64_t* __restrict__ lb = nullptr,
                                                    int hdr_words = 0, int prefix_bits = 0) {
     __shared__ uint32_t lds[1024 / 64 + 1];
+    // the chunk's counts and offsets staged through LDS so that loads and stores are coalesced (a thread's SC_PER
+    // consecutive tiles straight from global touched a line per lane: 17-22 us for C3's 9.2k tiles), padded rows
+    // against bank conflicts
+    __shared__ uint32_t sg_l[1024 * (SC_PER + 1)], se_l[1024 * (SC_PER + 1)];
     const int64_t ntiles = ((n_dev ? (int64_t)*n_dev : n_host) + TK_TILE - 1) / TK_TILE;
     uint32_t cg = 0, ce = 0;
     for (int64_t b = 0; b < ntiles; b += 1024 * SC_PER) {
         const int64_t i0 = b + (int64_t)threadIdx.x * SC_PER;
+        if (b > 0) __syncthreads();   // the previous chunk's LDS reads are done
+#pragma unroll
+        for (int j = 0; j < SC_PER; j++) {
+            const int64_t k = (int64_t)j * 1024 + threadIdx.x;   // chunk-relative tile, coalesced over threads
+            const uint32_t row = (uint32_t)(k / SC_PER), col = (uint32_t)(k % SC_PER);
+            sg_l[row * (SC_PER + 1) + col] = b + k < ntiles ? gt[b + k] : 0u;
+            se_l[row * (SC_PER + 1) + col] = b + k < ntiles ? eq[b + k] : 0u;
+        }
+        __syncthreads();
         uint32_t g[SC_PER], e[SC_PER], sg = 0, se = 0;
 #pragma unroll
         for (int j = 0; j < SC_PER; j++) {
-            g[j] = i0 + j < ntiles ? gt[i0 + j] : 0u;
-            e[j] = i0 + j < ntiles ? eq[i0 + j] : 0u;
+            g[j] = sg_l[threadIdx.x * (SC_PER + 1) + j];
+            e[j] = se_l[threadIdx.x * (SC_PER + 1) + j];
             sg += g[j];
             se += e[j];
         }
@@ -432,13 +445,22 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
         uint32_t xg = block_excl_scan<1024>(sg, lds, &tg) + cg;
         uint32_t xe = block_excl_scan<1024>(se, lds, &te) + ce;
 #pragma unroll
-        for (int j = 0; j < SC_PER; j++)
-            if (i0 + j < ntiles) {
-                gt[i0 + j] = xg;
-                eq[i0 + j] = xe;
-                xg += g[j];
-                xe += e[j];
+        for (int j = 0; j < SC_PER; j++) {   // the offsets back through LDS: coalesced stores
+            sg_l[threadIdx.x * (SC_PER + 1) + j] = xg;
+            se_l[threadIdx.x * (SC_PER + 1) + j] = xe;
+            xg += g[j];
+            xe += e[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SC_PER; j++) {
+            const int64_t k = (int64_t)j * 1024 + threadIdx.x;
+            const uint32_t row = (uint32_t)(k / SC_PER), col = (uint32_t)(k % SC_PER);
+            if (b + k < ntiles) {
+                gt[b + k] = sg_l[row * (SC_PER + 1) + col];
+                eq[b + k] = se_l[row * (SC_PER + 1) + col];
             }
+        }
         cg += tg;
         ce += te;
     }
