@@ -19,6 +19,8 @@
 //      32 bits, 59 at 36: profiles/analysis/keystats.c, turn 12); 6. an exact fix-up re-orders any run
 //      of equal prefixes that still holds different keys, stably by the full key.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "sb_block.h"
 #include "sb_internal.h"
@@ -79,7 +81,8 @@ enum : int {
     ST_FXN,     // fix-up: flagged positions (prefix equal to the predecessor's, key not)
     ST_FXI,     // fix-up: work counter over the flagged positions
     ST_HARR,    // select histogram: blocks arrived (the last one picks: SB_TK_PICK_FUSED)
-    ST_HIST = 20,
+    ST_T2,      // fused first pass: the lowest kept key two selects back (kept across selects)
+    ST_HIST = 24,
     ST_WORDS = ST_HIST + SEL_BINS
 };
 
@@ -87,7 +90,7 @@ __device__ __forceinline__ uint64_t hi_bits(uint64_t k, uint64_t sh) { return sh
 
 __device__ __forceinline__ void tk_init_body(uint64_t* st, int64_t keep, int keep_range, int fused) {
     const int t = threadIdx.x;
-    if (t < ST_HIST && (t > ST_MAX || !keep_range) && !(fused && t == ST_FBASE)) st[t] = 0;
+    if (t < ST_HIST && t != ST_T2 && (t > ST_MAX || !keep_range) && !(fused && t == ST_FBASE)) st[t] = 0;
     __syncthreads();
     if (t == 0) {
         if (!keep_range) st[ST_MIN] = ~0ull;
@@ -1234,8 +1237,13 @@ __global__ void k_tk_range_reset(uint64_t* st, int fused, int off_window, uint32
     if (threadIdx.x == 0) {
         if (fused) {
             int64_t b0;
-            if (SB_SEL_FSH == 47) {   // round 3: the top bin two binades above the previous maximum
-                b0 = (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
+            if (SB_SEL_FSH == 47) {   // 64 binades centred on the threshold two selects back (ST_T2).  Round 3 hung the
+                                      // window two binades above the previous maximum; C4's players alternate, so its
+                                      // threshold flips sign every turn (order keys 2^63 apart) and that, or the
+                                      // previous threshold, left C4 in fallback
+                b0 = st[ST_T2] ? (int64_t)(st[ST_T2] >> 47) - SEL_BINS / 2
+                               : (int64_t)(st[ST_MAX] >> 47) + 64 - (SEL_BINS - 1);
+                st[ST_T2] = st[ST_SLO];   // the previous select's lowest kept key: two selects back at the next reset
             } else {   // half a binade below the previous threshold (ST_SLO: the lowest kept key) to 1.5 above
                 const uint64_t ref = st[ST_SLO] ? st[ST_SLO] : st[ST_MAX];
                 b0 = (int64_t)(ref >> SB_SEL_FSH) - (int64_t)((1ull << 52) >> SB_SEL_FSH) / 2;
@@ -1420,6 +1428,19 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
     if (!fxo)
         hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
+    static const bool stats = getenv("SB_TOPK_STATS") != nullptr;   // diagnostics: the select's counts (a host wait)
+    if (stats && selected) {
+        uint64_t h[ST_HIST];
+        SB_HIP(hipMemcpyAsync(h, stv, sizeof(h), hipMemcpyDeviceToHost, st));
+        SB_HIP(hipStreamSynchronize(st));
+        fprintf(stderr, "topk n %lld keep %lld: above %llu candidates %llu above-T %llu ties %llu sh %llu fallback %llu "
+                "bins: fbase %llu min %llu max %llu T %llu\n",
+                (long long)n, (long long)keep, (unsigned long long)h[ST_A], (unsigned long long)h[ST_NC],
+                (unsigned long long)h[ST_G2], (unsigned long long)h[ST_E2], (unsigned long long)h[ST_SH],
+                (unsigned long long)h[ST_FALLBACK], (unsigned long long)h[ST_FBASE],
+                (unsigned long long)(h[ST_MIN] >> 47), (unsigned long long)(h[ST_MAX] >> 47),
+                (unsigned long long)(h[ST_SLO] >> 47));
+    }
     return m;
 }
 
