@@ -866,6 +866,7 @@ struct Engine {
     DBuf<uint8_t> digit;
     DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
     DBuf<uint16_t> mrj;                   // card-set records: (parent in chunk << 8) | move, at the record's slot
+    DBuf<uint8_t> snv;                    // sharded emission: each survivor's noise draw (3-word kept records)
     DBuf<uint32_t> mcrec;                 // card-set records per 64-parent chunk of the expand list
     // visited-set growth (grow_table): largest raw children per parent seen so far, tables rebuilt
     double raw_ratio = 32.0;
@@ -1782,6 +1783,7 @@ void sb_destroy(sb_engine* h) {
     E.digit.release();
     E.rdsc.release();
     E.mrj.release();
+    E.snv.release();
     E.mcrec.release();
     if (E.s_claim) (void)hipStreamSynchronize(E.s_claim);
     E.ks_rdr.release();

@@ -1210,7 +1210,8 @@ class HipBackend:
     def pack_kept(self, n_rows):
         """Kept records grouped by destination into a buffer of n_rows (>= the kept count: the local
         next_queue size), enqueued before the counts reach the host."""
-        rec = torch.empty((max(int(n_rows), 1), 4), dtype=torch.int64, device=self.device)
+        # 4 words (lo, hi, parent | position, key) with owner emission, else 3 (lo, hi, parent | draw): re-scored
+        rec = torch.empty((max(int(n_rows), 1), 4 if self.oe else 3), dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None), 'sbd_pack_kept')
         return rec
 
