@@ -105,6 +105,7 @@ struct TopkScratch {
     DBuf<uint64_t> small;           // select state + histogram
     DBuf<uint32_t> fx_list;         // sort fix-up: flagged positions
     DBuf<uint32_t> fx_mark;         // sort fix-up: run claims (epoch stamps)
+    DBuf<uint32_t> fx_list2;        // sort fix-up: runs with too many distinct keys for a wave (k_fx_fix)
     DBuf<uint32_t> osh_part;        // sort digit histograms: one row per k_os_hist block (two-stage flush)
     DBuf<uint32_t> tkh_part;        // select histograms: one row per k_tk_hist block (two-stage flush)
     DBuf<uint64_t> sk;              // select: staged first-partition keys (one TK_TILE region per tile)
@@ -128,9 +129,9 @@ struct TopkScratch {
 int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t* out_idx, TopkScratch& s,
                          hipStream_t st, bool range_ready = false, uint32_t* err = nullptr, bool fused = false,
                          const uint32_t* payload = nullptr, bool full_key = false);
-// fill_ff (optional): 256 u32 words set to ~0 by the same launch (the gather's per-pts first-rank table)
+// fill_ff (optional): fill_n u32 words set to ~0 by the same launch (the gather's per-pts first-rank table)
 // fused first select pass (the producer's histogram): bins of key >> SB_SEL_FSH over a 2048-bin window.  47 (default):
-// 1/32-binade bins below the previous maximum, then a second pass over all keys before the partition.  42 (A/B,
+// 1/32-binade bins around the threshold two selects back, then a second pass over all keys before the partition.  42 (A/B,
 // rejected): 1/1024-binade bins around the previous threshold and no second pass — but C3's scores are so
 // discrete (≈115k distinct values in the kept 4M) that the threshold's bin still holds millions of keys, and
 // copying them as candidates costs more than the pass it saves (select 0.578 -> 0.578-0.588 ms; stage 89 -> 130-143

@@ -82,6 +82,8 @@ enum : int {
     ST_FXI,     // fix-up: work counter over the flagged positions
     ST_HARR,    // select histogram: blocks arrived (the last one picks: SB_TK_PICK_FUSED)
     ST_T2,      // fused first pass: the lowest kept key two selects back (kept across selects)
+    ST_FX2N,    // fix-up: runs deferred by k_fx_wave to k_fx_fix
+    ST_FX2I,    // fix-up: work counter over them
     ST_HIST = 24,
     ST_WORDS = ST_HIST + SEL_BINS
 };
@@ -698,6 +700,8 @@ __device__ __forceinline__ void tk_sortsetup_body(uint64_t* st, int selected, in
     st[ST_SH32] = topk > (uint64_t)prefix_bits ? topk - prefix_bits : 0;   // the sort orders the top varying bits
     st[ST_FXN] = 0;
     st[ST_FXI] = 0;
+    st[ST_FX2N] = 0;
+    st[ST_FX2I] = 0;
 }
 __global__ void k_tk_sortsetup(uint64_t* st, int selected, int prefix_bits) { tk_sortsetup_body(st, selected, prefix_bits); }
 
@@ -1048,15 +1052,19 @@ __global__ __launch_bounds__(256) void k_fx_mark(const uint64_t* k0, const uint6
     }
 }
 
+// deferred (k_fx_wave ran first): list = the starts of the runs it claimed but left (too many distinct keys),
+// counted in ST_FX2N — no claim here
 __global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint32_t* out, int64_t m,
                                                   uint64_t* st, const uint32_t* __restrict__ list,
-                                                  uint32_t* __restrict__ runmark, uint32_t epoch, uint32_t* err) {
+                                                  uint32_t* __restrict__ runmark, uint32_t epoch, uint32_t* err,
+                                                  int deferred = 0) {
     const int P = sort_passes(st);
     uint64_t* kf = (P & 1) ? k1 : k0;
     uint32_t* vf = (P & 1) ? v1 : v0;
     uint64_t* ka = (P & 1) ? k0 : k1;   // the other buffer: scratch for the run
     uint32_t* va = (P & 1) ? v0 : v1;
-    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32], nflag = st[ST_FXN];
+    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32], nflag = st[deferred ? ST_FX2N : ST_FXN];
+    const int ticket = deferred ? ST_FX2I : ST_FXI;
     __shared__ uint64_t skey[FX_SET];
     __shared__ uint32_t scnt[FX_SET], sstart[FX_SET];
     __shared__ uint64_t lkey[FX_LIST];
@@ -1065,7 +1073,7 @@ __global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, ui
     __shared__ uint32_t go, nd;
     const int t = threadIdx.x;
     for (;;) {
-        if (t == 0) sj = atomicAdd((unsigned long long*)&st[ST_FXI], 1ull);
+        if (t == 0) sj = atomicAdd((unsigned long long*)&st[ticket], 1ull);
         __syncthreads();
         const uint64_t j = sj;
         if (j >= nflag) return;
@@ -1094,8 +1102,8 @@ __global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, ui
         // claim the run once per sort call (several flagged positions can share it)
         if (t == 0) {
             uint32_t old = runmark[sa];
-            go = 0;
-            while (old != epoch) {
+            go = deferred;   // a deferred run was claimed by the wave that listed it
+            while (!deferred && old != epoch) {
                 const uint32_t got = atomicCAS(&runmark[sa], old, epoch);
                 if (got == old) {
                     go = 1;
@@ -1195,6 +1203,113 @@ __global__ __launch_bounds__(FX_NT) void k_fx_fix(uint64_t* k0, uint32_t* v0, ui
     }
 }
 
+// Fix-up, a wave per flagged position (ahead of k_fx_fix): the wave finds the run of equal prefixes around it
+// (64 positions per step), claims it, lists its distinct keys with their counts (ballots: a run holds a
+// handful), and places every element at start(its key, descending) + its rank among equal keys in run order,
+// writing the payloads to out.  A run with more than FXW_MAXD distinct keys goes to k_fx_fix (deferred).
+// Every run is worked on by one wave, in parallel: a workgroup per run in turn (k_fx_fix alone) made prefixes
+// shorter than 40 bits cost more than the LSD pass they save.
+constexpr int FXW_MAXD = 32;
+__global__ __launch_bounds__(256) void k_fx_wave(const uint64_t* __restrict__ k0, const uint32_t* __restrict__ v0,
+                                                 const uint64_t* __restrict__ k1, const uint32_t* __restrict__ v1,
+                                                 uint32_t* __restrict__ out, int64_t m, uint64_t* st,
+                                                 const uint32_t* __restrict__ list, uint32_t* __restrict__ list2,
+                                                 uint32_t* __restrict__ runmark, uint32_t epoch) {
+    const int P = sort_passes(st);
+    const uint64_t* kf = (P & 1) ? k1 : k0;
+    const uint32_t* vf = (P & 1) ? v1 : v0;
+    const uint64_t slo = st[ST_SLO], sh = st[ST_SH32], nflag = st[ST_FXN];
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lanemask_lt();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < (int64_t)nflag; j += nw) {
+        const int64_t i = list[j];
+        const uint64_t pre = sort_prefix(kf[i], slo, sh);
+        int64_t a = -1, b = -1;
+        for (int64_t base = i - 1; a < 0; base -= 64) {   // lane l looks at base - l
+            const int64_t q = base - lane;
+            const bool same = q >= 0 && sort_prefix(kf[q], slo, sh) == pre;
+            const uint64_t ns = __ballot(!same);
+            if (ns) a = base - __builtin_ctzll(ns) + 1;
+        }
+        for (int64_t base = i + 1; b < 0; base += 64) {
+            const int64_t q = base + lane;
+            const bool same = q < m && sort_prefix(kf[q], slo, sh) == pre;
+            const uint64_t ns = __ballot(!same);
+            if (ns) b = base + __builtin_ctzll(ns);
+        }
+        int go = 0;
+        if (lane == 0) {
+            uint32_t old = runmark[a];
+            while (old != epoch) {
+                const uint32_t got = atomicCAS(&runmark[a], old, epoch);
+                if (got == old) {
+                    go = 1;
+                    break;
+                }
+                old = got;
+            }
+        }
+        if (!__builtin_amdgcn_readfirstlane(go)) continue;
+        // distinct keys: lane d holds the d-th one found and its count
+        uint64_t dk = 0;
+        uint32_t dc = 0;
+        int nd = 0;
+        bool over = false;
+        for (int64_t q0 = a; q0 < b && !over; q0 += 64) {
+            const int64_t q = q0 + lane;
+            const bool valid = q < b;
+            const uint64_t k = valid ? kf[q] : 0ull;
+            uint64_t left = __ballot(valid);
+            for (int d = 0; d < nd; d++) {
+                const uint64_t kd = __shfl(dk, d, 64);
+                const uint64_t mm = __ballot(valid && k == kd);
+                if (lane == d) dc += (uint32_t)__popcll(mm);
+                left &= ~mm;
+            }
+            while (left) {
+                if (nd == FXW_MAXD) {
+                    over = true;
+                    break;
+                }
+                const uint64_t kd = __shfl(k, __builtin_ctzll(left), 64);
+                const uint64_t mm = __ballot(valid && k == kd);
+                if (lane == nd) {
+                    dk = kd;
+                    dc = (uint32_t)__popcll(mm);
+                }
+                nd++;
+                left &= ~mm;
+            }
+        }
+        if (over) {   // claimed: k_fx_fix places it without claiming
+            if (lane == 0) list2[atomicAdd((unsigned long long*)&st[ST_FX2N], 1ull)] = (uint32_t)a;
+            continue;
+        }
+        uint32_t start = 0, run = 0;   // lane d: elements with a larger key; elements of key d placed so far
+        for (int d = 0; d < nd; d++) {
+            const uint64_t kd = __shfl(dk, d, 64);
+            const uint32_t cd = (uint32_t)__shfl((int)dc, d, 64);
+            if (lane < nd && kd > dk) start += cd;
+        }
+        for (int64_t q0 = a; q0 < b; q0 += 64) {
+            const int64_t q = q0 + lane;
+            const bool valid = q < b;
+            const uint64_t k = valid ? kf[q] : 0ull;
+            const uint32_t v = valid ? vf[q] : 0u;
+            int64_t dst = -1;
+            for (int d = 0; d < nd; d++) {
+                const uint64_t kd = __shfl(dk, d, 64);
+                const uint64_t mm = __ballot(valid && k == kd);
+                const uint32_t sd = (uint32_t)__shfl((int)start, d, 64), rd = (uint32_t)__shfl((int)run, d, 64);
+                if (valid && k == kd) dst = a + sd + rd + __popcll(mm & lt);
+                if (lane == d) run += (uint32_t)__popcll(mm);
+            }
+            if (valid) out[dst] = v;
+        }
+    }
+}
+
 __global__ void k_copy_idx(const uint32_t* v0, const uint32_t* v1, const uint64_t* st, uint32_t* out, int64_t n,
                            const uint64_t* lb, uint32_t* err) {
     if (err && blockIdx.x == 0 && threadIdx.x == 0 && lb[OS_ERR]) atomicOr(err, 4u);
@@ -1222,6 +1337,7 @@ void TopkScratch::release() {
     small.release();
     fx_list.release();
     fx_mark.release();
+    fx_list2.release();
     osh_part.release();
     tkh_part.release();
     sk.release();
@@ -1297,8 +1413,14 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
                          hipStream_t st, bool range_ready, uint32_t* err, bool fused, const uint32_t* payload,
                          bool full_key) {
     if (n <= 0 || keep <= 0) return 0;
-    const int prefix_bits = full_key ? 64 : OS_PREFIX_BITS;
     const int64_t m = n < keep ? n : keep;
+    // up to 2^21 kept keys a 30-bit prefix (three LSD passes): prefix collisions fall with the square of the count —
+    // C4's 1M kept keys flag none at 30 bits, C3's 4M flag 40-90k and their fix-up costs more than the fourth pass
+    // saves (profiles/r4/s2/sort_prefix_ab.txt)
+#ifndef SB_SORT_SMALL_M
+#define SB_SORT_SMALL_M (1 << 21)
+#endif
+    const int prefix_bits = full_key ? 64 : (m <= SB_SORT_SMALL_M && OS_PREFIX_BITS > 30 ? 30 : OS_PREFIX_BITS);
     s.k0.ensure(m);
     s.k1.ensure(m);
     s.v0.ensure(m);
@@ -1423,8 +1545,19 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #ifndef SB_FX_GRID
 #define SB_FX_GRID 64   // fix-up workgroups (each takes flagged positions until none are left)
 #endif
-    hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, fxo, m, stv, s.fx_list.p,
-                       s.fx_mark.p, epoch, err);
+#ifndef SB_FX_WAVE
+#define SB_FX_WAVE 1   // a wave per run first (k_fx_wave), k_fx_fix only for runs it defers
+#endif
+    if (SB_FX_WAVE && fxo) {
+        s.fx_list2.ensure((size_t)m);
+        hipLaunchKernelGGL(k_fx_wave, dim3(1024), dim3(256), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, fxo, m, stv, s.fx_list.p,
+                           s.fx_list2.p, s.fx_mark.p, epoch);
+        hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, fxo, m, stv,
+                           s.fx_list2.p, s.fx_mark.p, epoch, err, 1);
+    } else {
+        hipLaunchKernelGGL(k_fx_fix, dim3(SB_FX_GRID), dim3(FX_NT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, fxo, m, stv,
+                           s.fx_list.p, s.fx_mark.p, epoch, err, 0);
+    }
     if (!fxo)
         hipLaunchKernelGGL(k_copy_idx, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, s.v1.p, stv, out_idx, m, s.os.p, err);
     SB_HIP(hipGetLastError());
@@ -1434,12 +1567,13 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
         SB_HIP(hipMemcpyAsync(h, stv, sizeof(h), hipMemcpyDeviceToHost, st));
         SB_HIP(hipStreamSynchronize(st));
         fprintf(stderr, "topk n %lld keep %lld: above %llu candidates %llu above-T %llu ties %llu sh %llu fallback %llu "
-                "bins: fbase %llu min %llu max %llu T %llu\n",
+                "bins: fbase %llu min %llu max %llu T %llu; sort passes %d, fix-up flagged %llu deferred %llu\n",
                 (long long)n, (long long)keep, (unsigned long long)h[ST_A], (unsigned long long)h[ST_NC],
                 (unsigned long long)h[ST_G2], (unsigned long long)h[ST_E2], (unsigned long long)h[ST_SH],
                 (unsigned long long)h[ST_FALLBACK], (unsigned long long)h[ST_FBASE],
                 (unsigned long long)(h[ST_MIN] >> 47), (unsigned long long)(h[ST_MAX] >> 47),
-                (unsigned long long)(h[ST_SLO] >> 47));
+                (unsigned long long)(h[ST_SLO] >> 47), (int)((h[ST_TOPK] - h[ST_SH32] + OS_D - 1) / OS_D),
+                (unsigned long long)h[ST_FXN], (unsigned long long)h[ST_FX2N]);
     }
     return m;
 }
