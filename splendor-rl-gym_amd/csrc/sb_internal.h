@@ -112,6 +112,9 @@ struct TopkScratch {
     DBuf<uint32_t> si;              // select: staged first-partition payloads
     uint32_t fx_epoch = 0;
     uint32_t os_epoch = 0;          // LSD sort look-back granule epochs (SB_OS_EPOCH)
+    uint64_t* h_nc = nullptr;       // pinned: the last select's candidate count (read without a wait: nc_ev)
+    hipEvent_t nc_ev = nullptr;
+    bool nc_pending = false;
     void release();
 };
 // Stable descending order of keys[0..n) (ties keep index order), first `keep` indices into out_idx.

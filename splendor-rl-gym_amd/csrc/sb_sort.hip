@@ -483,6 +483,118 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
     }
 }
 
+// The select's tail in one workgroup (small candidate sets: C4's hold a few thousand keys): every remaining
+// digit over the candidates (LDS histogram, in-block pick), then the stable partition of the candidates above T
+// (group 2) and the first NEED ties (group 3), the totals and bases, and the sort's setup — in place of up to four
+// histogram + pick launch pairs and the count / scan / write launches, each ≈4.5 us even when it has nothing to do.
+// Correct for any candidate count; the host picks it from the previous select's count (a large jump only costs time).
+constexpr int TT_NT = 1024;
+constexpr int TT_U = 8;   // candidate loads in flight per thread
+__global__ __launch_bounds__(TT_NT) void k_tk_tail(const uint64_t* __restrict__ ck, const uint32_t* __restrict__ ci,
+                                                   uint64_t* st, uint64_t* __restrict__ gk, uint32_t* __restrict__ gi,
+                                                   uint64_t* __restrict__ lb, int hdr_words, int prefix_bits) {
+    __shared__ uint32_t h[SEL_BINS];
+    __shared__ uint32_t lds[TT_NT / 64 + 1];
+    __shared__ uint64_t s_prefix, s_sh, s_need;
+    __shared__ int s_done;
+    const int t = threadIdx.x;
+    const int64_t nc = (int64_t)st[ST_NC];
+    if (t == 0) {
+        s_prefix = st[ST_PREFIX];
+        s_sh = st[ST_SH];
+        s_need = st[ST_NEED];
+        s_done = (int)st[ST_DONE];
+    }
+    __syncthreads();
+    for (int it = 0; it < 8 && !s_done && s_sh > 0; it++) {   // at most ceil(64 / SEL_D) digits
+        const uint64_t sh = s_sh, prefix = s_prefix, need = s_need;
+        const uint64_t d = sh < SEL_D ? sh : SEL_D;
+        const uint64_t dmask = (1ull << d) - 1;
+        for (int i = t; i < SEL_BINS; i += TT_NT) h[i] = 0;
+        __syncthreads();
+        for (int64_t i0 = t; i0 < nc; i0 += (int64_t)TT_NT * TT_U) {
+            uint64_t kk[TT_U];
+#pragma unroll
+            for (int u = 0; u < TT_U; u++) kk[u] = i0 + u * TT_NT < nc ? ck[i0 + u * TT_NT] : 0ull;
+#pragma unroll
+            for (int u = 0; u < TT_U; u++)
+                if (i0 + u * TT_NT < nc && hi_bits(kk[u], sh) == prefix) atomicAdd(&h[(kk[u] >> (sh - d)) & dmask], 1u);
+        }
+        __syncthreads();
+        const int nb = 1 << d;
+        constexpr int PER = SEL_BINS / TT_NT;
+        uint32_t c[PER], loc = 0;
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int b = nb - 1 - (t * PER + j);
+            c[j] = b >= 0 ? h[b] : 0u;
+            loc += c[j];
+        }
+        uint32_t tot;
+        uint64_t cum = block_excl_scan<TT_NT>(loc, lds, &tot);
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int b = nb - 1 - (t * PER + j);
+            if (b >= 0 && c[j] && cum < need && cum + c[j] >= need) {
+                s_need = need - cum;
+                s_prefix = (prefix << d) | (uint64_t)b;
+                s_sh = sh - d;
+                s_done = (c[j] == need - cum) || (sh - d == 0);
+            }
+            cum += c[j];
+        }
+        __syncthreads();
+    }
+    const uint64_t sh = s_sh, prefix = s_prefix, need = s_need;
+    // group 2's size first (group 3 starts after it), then both groups in index order, 1024 candidates a round
+    uint32_t above = 0;
+    for (int64_t i = t; i < nc; i += TT_NT) above += hi_bits(ck[i], sh) > prefix;
+    uint32_t g2;
+    (void)block_excl_scan<TT_NT>(above, lds, &g2);
+    const uint64_t base2 = st[ST_A], base3 = base2 + g2;
+    uint64_t run_g = 0, run_e = 0;
+    for (int64_t b0 = 0; b0 < nc; b0 += TT_NT) {
+        const int64_t i = b0 + t;
+        uint64_t k = 0;
+        bool g = false, e = false;
+        if (i < nc) {
+            k = ck[i];
+            const uint64_t hb = hi_bits(k, sh);
+            g = hb > prefix;
+            e = hb == prefix;
+        }
+        uint32_t totv;
+        const uint32_t x = block_excl_scan<TT_NT>((uint32_t)g | ((uint32_t)e << 16), lds, &totv);
+        if (g) {
+            const uint64_t o = base2 + run_g + (x & 0xFFFFu);
+            gk[o] = k;
+            gi[o] = ci[i];
+        } else if (e) {
+            const uint64_t re = run_e + (x >> 16);
+            if (re < need) {
+                gk[base3 + re] = k;
+                gi[base3 + re] = ci[i];
+            }
+        }
+        run_g += totv & 0xFFFFu;
+        run_e += totv >> 16;
+    }
+    __syncthreads();
+    if (t == 0) {
+        st[ST_PREFIX] = prefix;
+        st[ST_SH] = sh;
+        st[ST_NEED] = need;
+        st[ST_DONE] = 1;
+        st[ST_G2] = g2;
+        st[ST_E2] = run_e;
+        st[ST_BASE2] = base2;
+        st[ST_BASE3] = base3;
+        if (lb) tk_sortsetup_body(st, 1, prefix_bits);
+    }
+    if (lb)
+        for (int i = t; i < hdr_words; i += TT_NT) lb[i] = 0;
+}
+
 // Order-preserving partition of a tile (4096 elements, striped: element r*256 + t is thread t's r-th):
 // all 16 keys of a thread are loaded up front; per round and wave a ballot per class; one scan over
 // the tile's 16 x 4 (round, wave) counts orders everything.  A block takes tiles in grid strides.
@@ -1338,6 +1450,11 @@ void TopkScratch::release() {
     fx_list.release();
     fx_mark.release();
     fx_list2.release();
+    if (h_nc) (void)hipHostFree(h_nc);
+    if (nc_ev) (void)hipEventDestroy(nc_ev);
+    h_nc = nullptr;
+    nc_ev = nullptr;
+    nc_pending = false;
     osh_part.release();
     tkh_part.release();
     sk.release();
@@ -1488,19 +1605,38 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
                                (const uint64_t*)nullptr, s.ck.p, s.ci.p, (const uint64_t*)nullptr,
                                (const uint64_t*)nullptr, payload);
         }
-        // remaining digits on the candidates (device-side count; passes after DONE exit at once)
+        // remaining digits on the candidates (device-side count; passes after DONE exit at once) — or the whole tail
+        // in one workgroup when the previous select's candidates were few (the pinned count, read without a wait)
+#ifndef SB_TK_TAIL_MAX
+#define SB_TK_TAIL_MAX 4096
+#endif
+        bool tail = false;
+        if (s.nc_pending && hipEventQuery(s.nc_ev) == hipSuccess) tail = *s.h_nc <= (uint64_t)SB_TK_TAIL_MAX;
         const uint64_t* nc = stv + ST_NC;
-        for (int pass = 0; pass < SEL_PASSES_C; pass++) {
-            tk_hist_pick(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, (unsigned)SB_TK_CAND_GRID), true);
+        if (tail) {
+            hipLaunchKernelGGL(k_tk_tail, dim3(1), dim3(TT_NT), 0, st, s.ck.p, s.ci.p, stv, s.k0.p, s.v0.p,
+                               SB_OS_EPOCH ? s.os.p : (uint64_t*)nullptr, (int)OS_HDR, prefix_bits);
+            sort_begun = SB_OS_EPOCH;
+        } else {
+            for (int pass = 0; pass < SEL_PASSES_C; pass++) {
+                tk_hist_pick(s, st, s.ck.p, n, nc, stv, 0, std::min(hg, (unsigned)SB_TK_CAND_GRID), true);
+            }
+            // candidates above T -> group 2, the first NEED ties -> group 3
+            hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
+            hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, nc, stv, (int)ST_G2,
+                               (int)ST_E2, 1, SB_OS_EPOCH ? s.os.p : (uint64_t*)nullptr, (int)OS_HDR, prefix_bits);
+            sort_begun = SB_OS_EPOCH;
+            hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
+                               s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
+                               stv + ST_NEED, (const uint32_t*)nullptr);
         }
-        // candidates above T -> group 2, the first NEED ties -> group 3
-        hipLaunchKernelGGL(k_tk_count, dim3(cg), dim3(TK_NT), 0, st, s.ck.p, n, nc, stv, s.tile_a.p, s.tile_b.p);
-        hipLaunchKernelGGL(k_tk_scan, dim3(1), dim3(1024), 0, st, s.tile_a.p, s.tile_b.p, n, nc, stv, (int)ST_G2,
-                           (int)ST_E2, 1, SB_OS_EPOCH ? s.os.p : (uint64_t*)nullptr, (int)OS_HDR, prefix_bits);
-        sort_begun = SB_OS_EPOCH;
-        hipLaunchKernelGGL(k_tk_write, dim3(wg), dim3(TK_NT), 0, st, s.ck.p, s.ci.p, n, nc, stv,
-                           s.tile_a.p, s.tile_b.p, s.k0.p, s.v0.p, stv + ST_BASE2, s.k0.p, s.v0.p, stv + ST_BASE3,
-                           stv + ST_NEED, (const uint32_t*)nullptr);
+        if (!s.h_nc) {
+            SB_HIP(hipHostMalloc((void**)&s.h_nc, 8, hipHostMallocDefault));
+            SB_HIP(hipEventCreateWithFlags(&s.nc_ev, hipEventDisableTiming));
+        }
+        SB_HIP(hipMemcpyAsync(s.h_nc, stv + ST_NC, 8, hipMemcpyDeviceToHost, st));
+        SB_HIP(hipEventRecord(s.nc_ev, st));
+        s.nc_pending = true;
     } else {
         hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, st, s.v0.p, keys, s.k0.p, m, payload);
     }
