@@ -106,6 +106,7 @@ struct TopkScratch {
     DBuf<uint32_t> fx_list;         // sort fix-up: flagged positions
     DBuf<uint32_t> fx_mark;         // sort fix-up: run claims (epoch stamps)
     DBuf<uint32_t> fx_list2;        // sort fix-up: runs with too many distinct keys for a wave (k_fx_fix)
+    DBuf<uint32_t> os_tcnt;         // LSD sort (two-level passes): per-digit tile counts, then their offsets
     DBuf<uint32_t> osh_part;        // sort digit histograms: one row per k_os_hist block (two-stage flush)
     DBuf<uint32_t> tkh_part;        // select histograms: one row per k_tk_hist block (two-stage flush)
     DBuf<uint64_t> sk;              // select: staged first-partition keys (one TK_TILE region per tile)

@@ -1038,9 +1038,13 @@ __device__ __forceinline__ void os_lookback(uint64_t* lb, int64_t tile, int p, c
 #define SB_OS_WAVES 0   // 0: the compiler's register choice (155 VGPRs: 3 waves per SIMD).  4 (128 VGPRs, a 104 B
                         // spill) measured slower: 257 -> 341 us per step (profiles/r3/s5/ab_sort_digits.txt)
 #endif
+// M (the pass's way to its tiles' offsets): 0 the decoupled look-back (default); 1 count only (each tile's per-digit
+// counts to tcnt[digit][tile], no scatter); 2 scatter with tcnt scanned over the tiles (k_os_tscan) — the
+// two-level variant (SB_OS_TWOLEVEL), measured slower: profiles/r4/s2/sort_twolevel_ab.txt
+template <int M>
 __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n,
                                                    int p, const uint64_t* __restrict__ st, uint64_t* __restrict__ lb,
-                                                   uint32_t ebase) {
+                                                   uint32_t ebase, uint32_t* __restrict__ tcnt) {
     if (p >= sort_passes(st)) return;
     const uint64_t* kin = (p & 1) ? k1 : k0;
     const uint32_t* vin = (p & 1) ? v1 : v0;
@@ -1058,10 +1062,11 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
     const uint64_t lt = lanemask_lt();
     const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * OS_B;
     for (int it = 0;; it++) {
-        if (t == 0) s_tile = (SB_OS_DBG & 4) ? (it ? 0xFFFFFFFFu : blockIdx.x) : atomicAdd(&ticket[p], 1u);   // DBG 4: block order
+        if (M == 0 && t == 0)
+            s_tile = (SB_OS_DBG & 4) ? (it ? 0xFFFFFFFFu : blockIdx.x) : atomicAdd(&ticket[p], 1u);   // DBG 4: block order
         for (int i = t; i < OS_NW * OS_B; i += OS_PNT) (&wcnt[0][0])[i] = 0;
         __syncthreads();
-        const int64_t tile = s_tile;
+        const int64_t tile = M == 0 ? (int64_t)s_tile : (int64_t)blockIdx.x + (int64_t)it * gridDim.x;
         if (tile >= ntiles) return;
         const int64_t base = tile * OS_TILE + (int64_t)w * (64 * OS_IPT) + l;
         uint64_t kk[OS_IPT];
@@ -1071,7 +1076,7 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
         for (int r = 0; r < OS_IPT; r++) {
             const int64_t i = base + (int64_t)r * 64;
             kk[r] = i < n ? kin[i] : 0ull;
-            vv[r] = i < n ? vin[i] : 0u;
+            vv[r] = M != 1 && i < n ? vin[i] : 0u;
         }
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
@@ -1106,7 +1111,18 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
             gv[k] = gh[d0 + k];
             gsum += gv[k];
         }
-        os_lookback(lb, tile, p, agg, d0, ebase, excl);
+        if constexpr (M == 1) {   // count only: the tile's per-digit counts, digit-major for the scan over tiles
+#pragma unroll
+            for (int k = 0; k < OS_DPT; k++) tcnt[(int64_t)(d0 + k) * ntiles + tile] = agg[k];
+            __syncthreads();   // the next tile rewrites wcnt
+            continue;
+        }
+        if constexpr (M == 2) {
+#pragma unroll
+            for (int k = 0; k < OS_DPT; k++) excl[k] = tcnt[(int64_t)(d0 + k) * ntiles + tile];
+        } else {
+            os_lookback(lb, tile, p, agg, d0, ebase, excl);
+        }
         uint32_t tot;
         uint32_t run = block_excl_scan<OS_PNT>(gsum, lds, &tot);   // global start of each digit
 #pragma unroll
@@ -1126,6 +1142,26 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
             }
         }
         __syncthreads();   // the next tile rewrites wcnt / sbase
+    }
+}
+
+// the per-digit counts of k_os_pass<1> scanned over the tiles in place (exclusive): a wave per digit, each lane
+// a contiguous run of tiles
+__global__ __launch_bounds__(256) void k_os_tscan(uint32_t* __restrict__ tcnt, int64_t ntiles, int p,
+                                                  const uint64_t* __restrict__ st) {
+    if (p >= sort_passes(st)) return;
+    const int lane = threadIdx.x & 63;
+    const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (d >= OS_B) return;
+    uint32_t* c = tcnt + (int64_t)d * ntiles;
+    const int64_t per = (ntiles + 63) / 64, a = lane * per, b = a + per < ntiles ? a + per : ntiles;
+    uint32_t sum = 0;
+    for (int64_t i = a; i < b; i++) sum += c[i];
+    uint32_t run = wave_incl_scan(sum) - sum;
+    for (int64_t i = a; i < b; i++) {
+        const uint32_t v = c[i];
+        c[i] = run;
+        run += v;
     }
 }
 
@@ -1450,6 +1486,7 @@ void TopkScratch::release() {
     fx_list.release();
     fx_mark.release();
     fx_list2.release();
+    os_tcnt.release();
     if (h_nc) (void)hipHostFree(h_nc);
     if (nc_ev) (void)hipEventDestroy(nc_ev);
     h_nc = nullptr;
@@ -1661,9 +1698,26 @@ int64_t topk_stable_desc(const uint64_t* keys, int64_t n, int64_t keep, uint32_t
 #define SB_OS_GRID 1u << 20   // blocks per pass at most (tiles beyond are taken by ticket)
 #endif
     const unsigned osg = (unsigned)std::min<int64_t>(ntiles, (int64_t)(SB_OS_GRID));
-    for (int p = 0; p < (prefix_bits + OS_D - 1) / OS_D; p++)   // passes beyond the varying bits exit at once
-        hipLaunchKernelGGL(k_os_pass, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
-                           stv, s.os.p, ebase);
+#ifndef SB_OS_TWOLEVEL
+#define SB_OS_TWOLEVEL 0   // tiles from which a pass counts, scans and scatters (three launches, no look-back).  A/B at
+                           // 256 (C3): count 19 + scan 5-7 + scatter 31-35 us per pass against ≈50 with the look-back,
+                           // and the first pass's scatter alone 75-78 (select 0.585 -> 0.62 ms): the look-back is not
+                           // what makes a pass slow, the scatter of 1024 digits is (profiles/r4/s2/sort_twolevel_ab.txt)
+#endif
+    const bool twolevel = SB_OS_TWOLEVEL > 0 && ntiles >= SB_OS_TWOLEVEL;
+    if (twolevel) s.os_tcnt.ensure((size_t)OS_B * (size_t)ntiles);
+    for (int p = 0; p < (prefix_bits + OS_D - 1) / OS_D; p++) {   // passes beyond the varying bits exit at once
+        if (twolevel) {
+            hipLaunchKernelGGL(k_os_pass<1>, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+                               stv, s.os.p, ebase, s.os_tcnt.p);
+            hipLaunchKernelGGL(k_os_tscan, dim3(OS_B / 4), dim3(256), 0, st, s.os_tcnt.p, ntiles, p, stv);
+            hipLaunchKernelGGL(k_os_pass<2>, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+                               stv, s.os.p, ebase, s.os_tcnt.p);
+        } else {
+            hipLaunchKernelGGL(k_os_pass<0>, dim3(osg), dim3(OS_PNT), 0, st, s.k0.p, s.v0.p, s.k1.p, s.v1.p, m, p,
+                               stv, s.os.p, ebase, (uint32_t*)nullptr);
+        }
+    }
     // exact order among keys that share their 32-bit prefix
     if (s.fx_mark.cap < (size_t)m) {   // run claims carry this call's epoch: zeroed only when (re)allocated
         s.fx_mark.ensure((size_t)m);

@@ -101,7 +101,8 @@ def test_device_scores_golden(tables, hid, name):
 def test_device_topk_stable():
     rng = np.random.default_rng(5)
     for n, keep, distinct in [(1, 1, 1), (1000, 10, 3), (50_000, 7_000, 40), (300_000, 300_000, 1000),
-                              (1_000_000, 123_457, 2500), (200_000, 1, 5), (70_000, 69_999, 2)]:
+                              (1_000_000, 123_457, 2500), (200_000, 1, 5), (70_000, 69_999, 2),
+                              (3_000_000, 2_600_000, 200_000)]:   # >= 256 sort tiles: the two-level passes
         vals = rng.choice(rng.random(distinct) * 1e4 + 0.01, n)
         keys = vals.astype(np.float64).view(np.uint64)
         exp = np.argsort(-vals, kind='stable')[:keep]
