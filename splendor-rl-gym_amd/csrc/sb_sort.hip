@@ -52,9 +52,15 @@ constexpr int64_t TK_COUNT_GRID = SB_TK_COUNT_GRID;
 #endif
 constexpr int64_t TK_WRITE_GRID = SB_TK_WRITE_GRID;           // candidate passes: ceil(64 / 11) upper bound
 #ifndef SB_SORT_PREFIX_BITS
-#define SB_SORT_PREFIX_BITS 40   // 64: the plain full-key LSD sort (A/B knob)
+#define SB_SORT_PREFIX_BITS 38   // 64: the plain full-key LSD sort (A/B knob).  38 = an 8-bit first digit + three
+                                 // 10-bit ones: the first pass scatters the prefix's lowest, uniformly spread bits,
+                                 // and 256 destinations per tile write longer runs than 1024 (that pass took 83-88 us
+                                 // against 48-54 for the others at 40 bits; profiles/r4/s2/sort_d0_ab.txt)
 #endif
 constexpr int OS_PREFIX_BITS = SB_SORT_PREFIX_BITS;
+#ifndef SB_OS_D
+#define SB_OS_D 10       // digit bits per LSD pass (see k_os_pass below)
+#endif
 #ifndef SB_OS_EPOCH
 #define SB_OS_EPOCH 1            // look-back granules stamped with a per-call epoch (no clearing memset per call)
 #endif
@@ -84,6 +90,7 @@ enum : int {
     ST_T2,      // fused first pass: the lowest kept key two selects back (kept across selects)
     ST_FX2N,    // fix-up: runs deferred by k_fx_wave to k_fx_fix
     ST_FX2I,    // fix-up: work counter over them
+    ST_D0,      // sort: bits of the first LSD digit (the prefix bits beyond whole OS_D digits)
     ST_HIST = 24,
     ST_WORDS = ST_HIST + SEL_BINS
 };
@@ -810,6 +817,7 @@ __device__ __forceinline__ void tk_sortsetup_body(uint64_t* st, int selected, in
     st[ST_SLO] = lo;
     st[ST_TOPK] = topk;
     st[ST_SH32] = topk > (uint64_t)prefix_bits ? topk - prefix_bits : 0;   // the sort orders the top varying bits
+    st[ST_D0] = (uint64_t)(prefix_bits % SB_OS_D ? prefix_bits % SB_OS_D : SB_OS_D);   // first digit: the bits beyond whole digits
     st[ST_FXN] = 0;
     st[ST_FXI] = 0;
     st[ST_FX2N] = 0;
@@ -881,7 +889,15 @@ __device__ __forceinline__ uint64_t os_poll(const uint64_t* p) {
     return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int sort_passes(const uint64_t* st) { return (int)((st[ST_TOPK] - st[ST_SH32] + OS_D - 1) / OS_D); }
+// digit p covers bits [os_shift(p), os_shift(p) + os_width(p)) of the prefix: the first is ST_D0 bits wide, the rest OS_D
+__device__ __forceinline__ int sort_passes(const uint64_t* st) {
+    const int64_t v = (int64_t)(st[ST_TOPK] - st[ST_SH32]), d0 = (int64_t)st[ST_D0];
+    return v <= 0 ? 0 : (v <= d0 ? 1 : 1 + (int)((v - d0 + OS_D - 1) / OS_D));
+}
+__device__ __forceinline__ int os_shift(const uint64_t* st, int p) { return p == 0 ? 0 : (int)st[ST_D0] + OS_D * (p - 1); }
+__device__ __forceinline__ uint32_t os_mask(const uint64_t* st, int p) {
+    return p == 0 ? (1u << (int)st[ST_D0]) - 1u : (uint32_t)(OS_B - 1);
+}
 __device__ __forceinline__ uint64_t sort_prefix(uint64_t k, uint64_t slo, uint64_t sh) { return (k - slo) >> sh; }
 
 // histograms of every needed digit over the m keys (first lane's bin wave-aggregated: high digits
@@ -929,7 +945,7 @@ __global__ __launch_bounds__(OSH_NT) void k_os_hist(const uint64_t* __restrict__
             const bool valid = i0 + r * stride < n;
             if (!__ballot(valid)) break;
             for (int p = 0; p < P; p++) {
-                const int b = valid ? (int)((kk[r] >> (OS_D * p)) & (OS_B - 1)) : -1;
+                const int b = valid ? (int)((kk[r] >> os_shift(st, p)) & os_mask(st, p)) : -1;
                 const uint64_t act = __ballot(b >= 0);
                 const int b0 = __shfl(b, __builtin_ctzll(act), 64);
                 const uint64_t same = __ballot(b == b0);
@@ -1057,7 +1073,8 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(lb + OS_TICKET);
     const int64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
-    const int shift = OS_D * p;
+    const int shift = os_shift(st, p);
+    const uint32_t dmask = os_mask(st, p);
     const uint64_t slo = st[ST_SLO], psh = st[ST_SH32];
     const uint64_t lt = lanemask_lt();
     const uint32_t* gh = reinterpret_cast<const uint32_t*>(lb) + p * OS_B;
@@ -1081,7 +1098,7 @@ __global__ __launch_bounds__(OS_PNT, SB_OS_WAVES) void k_os_pass(uint64_t* k0, u
 #pragma unroll
         for (int r = 0; r < OS_IPT; r++) {
             const bool valid = base + (int64_t)r * 64 < n;
-            const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & (OS_B - 1));
+            const uint32_t d = (uint32_t)(((~sort_prefix(kk[r], slo, psh)) >> shift) & dmask);
             uint64_t peers = __ballot(valid);
 #pragma unroll
             for (int b = 0; b < OS_D; b++) {
