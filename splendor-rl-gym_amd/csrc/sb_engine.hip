@@ -867,6 +867,7 @@ struct Engine {
     DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
     DBuf<uint16_t> mrj;                   // card-set records: (parent in chunk << 8) | move, at the record's slot
     DBuf<uint8_t> snv;                    // sharded emission: each survivor's noise draw (3-word kept records)
+    DBuf<uint64_t> rkey2;                 // owner emission: received records' re-scored keys, arrival order
     bool sdesc = false, sdesc32 = false;  // sharded emission wrote descriptors (4-byte when sdesc32) into nlo
     int64_t sdesc_goff = 0;               // ... global ranks: the slice's parents start at this one
     DBuf<uint32_t> mcrec;                 // card-set records per 64-parent chunk of the expand list
@@ -1786,6 +1787,7 @@ void sb_destroy(sb_engine* h) {
     E.rdsc.release();
     E.mrj.release();
     E.snv.release();
+    E.rkey2.release();
     E.mcrec.release();
     if (E.s_claim) (void)hipStreamSynchronize(E.s_claim);
     E.ks_rdr.release();

@@ -1210,8 +1210,9 @@ class HipBackend:
     def pack_kept(self, n_rows):
         """Kept records grouped by destination into a buffer of n_rows (>= the kept count: the local
         next_queue size), enqueued before the counts reach the host."""
-        # 4 words (lo, hi, parent | position, key) with owner emission, else 3 (lo, hi, parent | draw): re-scored
-        rec = torch.empty((max(int(n_rows), 1), 4 if self.oe else 3), dtype=torch.int64, device=self.device)
+        # 3 words (lo, hi, parent | draw << 32; with owner emission parent | draw << 25 | position << 32): the
+        # receiver re-scores them
+        rec = torch.empty((max(int(n_rows), 1), 3), dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None), 'sbd_pack_kept')
         return rec
 
