@@ -89,6 +89,9 @@ def main(args):
     torch.cuda.set_device(dev)
     dist.init_process_group(backend, device_id=torch.device('cuda', dev) if backend == 'nccl' else None)
     rank, world = dist.get_rank(), dist.get_world_size()
+    # distinct physical devices under this world: ranks share a GPU only when wrapped (gloo tests, share)
+    n_phys = min(world, max(ndev, 1)) if share else world
+    ranks_per_gpu = -(-world // n_phys)
     if world != args.gpus and not (args.gpus == 1 and os.environ.get('SB_FORCE_DIST') == '1'):
         raise RuntimeError(f'--gpus {args.gpus} but the launcher started a world of {world}')
     W = args.width * world
@@ -157,8 +160,12 @@ def main(args):
             'config': {'workload': f'speedrun goal_pts={GOAL} -u -H {args.heuristic} beam_width={W} '
                                    f'({args.width} per GPU; C5 at 8 GPUs x 4M)',
                        'beam_width': W, 'heuristic': args.heuristic, 'seed': args.seed,
-                       'parallelism': f'beam sharded over {world} GPUs ({backend}); trail owned by '
-                                      + ('card set (parents migrate to their owners)'
+                       'physical_gpus': n_phys, 'ranks_per_gpu': ranks_per_gpu, 'shared_gpu': ranks_per_gpu > 1,
+                       'parallelism': (f'beam sharded over {world} ranks on {n_phys} GPU(s) ({backend}'
+                                       + (f', {ranks_per_gpu} ranks per GPU: not a multi-GPU measurement' if ranks_per_gpu > 1
+                                          else '') + '); trail owned by ')
+                                      + ('card set (parents migrate to their owners; NOT bit-exact by construction: '
+                                         'two card sets with an equal 64-bit key are both kept, DESIGN.md §6)'
                                          if world > 1 and (HipBackend.MIG or int(os.environ.get('SB_DIST_FLAGS', '0')) & 256)
                                          else 'key hash'),
                        'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
@@ -194,6 +201,10 @@ def main(args):
                                'algorithmic_bytes_per_step': int(abytes),
                                'whole_step': {'model': 'SURVEY §8d per GPU', 'achieved': round(gbs / world, 2),
                                               'frac': round(gbs / world / HBM_PEAK_GBS, 5)}}
+            if ranks_per_gpu > 1:   # the launch time includes the other ranks' work on the same device
+                out['roofline']['per_gpu_valid'] = False
+                out['roofline']['note'] = (f'{ranks_per_gpu} ranks share each GPU: the key kernel\'s event time '
+                                           'includes contention from the other ranks, so this is not a per-GPU roofline')
             pm = keypass_pmc(kname)
             if pm:
                 out['roofline']['traffic'] = pm['hbm_bytes_per_step']

@@ -68,7 +68,8 @@ typedef struct {
                                   pass gives every key (with bit 8: every card set) to rank 0 (parts that
                                   send no records; results unchanged); bit 8: card-set ownership of the
                                   sharded trail (sbd_mig_*, world_size > 1); bit 9 (with bit 8): owner
-                                  emission (sbd_oe_*) */
+                                  emission (sbd_oe_*); bit 10 (test): the pipelined turn's receive bound starts at
+                                  1024 records, so the host grows it (sbd_grow_receive) every turn */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -172,6 +173,10 @@ const char* sb_build_id(void);
 int sb_debug_successors(int32_t device, const uint64_t* lo, const uint64_t* hi, int64_t n,
                         uint64_t* out_lo, uint64_t* out_hi, uint64_t* out_key, int32_t* out_count);
 /* n tempered MT19937 words continuing from mt_state625 (device jump-ahead producers: 256 x 1 twist). */
+/* one device allocation through the engine's allocator, then freed: on failure (SB_ERR_CAPACITY when out of memory)
+ * sb_last_error names what, the bytes requested and the HBM free, as every engine allocation does;
+ * SB_DEBUG_HBM_LIMIT=<bytes> in the environment fails any single request above it (tests) */
+int sb_debug_alloc(uint64_t bytes);
 int sb_debug_mt_words(int32_t device, const uint32_t* mt_state625, int64_t n, uint32_t* out);
 /* same with `producers` (power of two) producers of `twists` twists per segment */
 int sb_debug_mt_words_cfg(int32_t device, const uint32_t* mt_state625, int64_t n, int32_t producers,
@@ -228,6 +233,10 @@ int sbd_part_counts(sb_engine* e, int32_t part, int64_t* owner_counts, int64_t* 
 int sbd_part_pack(sb_engine* e, int32_t part, uint64_t* d_key, int64_t send_base);
 int sbd_set_claim_stream(sb_engine* e, void* stream);
 int sbd_owner_total(sb_engine* e, int64_t n_total);
+/* the turn's received records will exceed the receive bound sbd_part_counts reported (an estimate from the raw
+ * ratio so far): drain this rank's streams and grow the lost bits (and the card-set answer tags) to hold n_needed,
+ * contents kept; *new_cap = the new bound.  The caller grows its answer buffer the same way. */
+int sbd_grow_receive(sb_engine* e, int64_t n_needed, int64_t* new_cap);
 /* world 1 (no records, no exchange to size): go on without waiting for the expansion; *n_raw is read by
  * sbd_raw_total after the caller's next wait on the engine stream (sbd_apply's count). */
 int sbd_expand_defer(sb_engine* e);

@@ -41,6 +41,38 @@ namespace sb {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+static std::string gib(double b) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.3f GiB", b / (double)(1ull << 30));
+    return buf;
+}
+
+std::string oom_message(const char* what, size_t bytes, hipError_t code) {
+    std::string m = std::string(what) + ": hipMalloc of " + gib((double)bytes) + " (" + std::to_string(bytes) +
+                    " bytes) failed: " + hipGetErrorString(code);
+    size_t freeb = 0, totalb = 0;
+    const hipError_t e = hipMemGetInfo(&freeb, &totalb);
+    if (e == hipSuccess) m += "; free HBM " + gib((double)freeb) + " of " + gib((double)totalb);
+    else m += std::string("; free HBM unknown (hipMemGetInfo: ") + hipGetErrorString(e) + ")";
+    (void)hipGetLastError();
+    return m;
+}
+
+void dev_malloc(void** p, size_t bytes, const char* what) {
+    static const char* lim = std::getenv("SB_DEBUG_HBM_LIMIT");
+    hipError_t e;
+    if (lim && (double)bytes > std::strtod(lim, nullptr)) {
+        e = hipErrorOutOfMemory;
+        throw HipError{e, oom_message(what, bytes, e) + " [SB_DEBUG_HBM_LIMIT=" + lim + "]"};
+    }
+    e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        throw HipError{e, oom_message(what, bytes, e)};
+    }
+}
+
 static Tables g_host_tables;
 static bool g_tables_ready = false;
 
@@ -943,7 +975,9 @@ static void grow_table(Engine& E, Entry*& tab, uint64_t& mask, double projected)
     while (ncap > cap && ncap * sizeof(Entry) + GROW_RESERVE > freeb) ncap >>= 1;
     if (ncap == cap) return;
     Entry* nt = nullptr;
-    SB_HIP(hipMalloc((void**)&nt, ncap * sizeof(Entry)));
+    const std::string what = "visited-set rebuild to " + std::to_string(ncap) + " slots (from " + std::to_string(cap) +
+                             "; free HBM at sizing " + gib((double)freeb) + ")";
+    dev_malloc((void**)&nt, ncap * sizeof(Entry), what.c_str());
     SB_HIP(hipMemsetAsync(nt, 0xFF, ncap * sizeof(Entry), E.s));
     hipLaunchKernelGGL(k_rehash, dim3(grid_cap((int64_t)std::min<uint64_t>(cap, 1ull << 40), 256, 1u << 16)), dim3(256), 0,
                        E.s, tab, cap, nt, ncap - 1, E.d_small + 1);
@@ -1395,6 +1429,17 @@ static int guarded(F&& f) {
 extern "C" {
 
 int sb_version(void) { return 1; }
+
+// one device allocation of `bytes` through the engine's allocator (then freed): its failure message, as every
+// engine allocation reports it (what, bytes requested, free HBM); SB_DEBUG_HBM_LIMIT forces the failure (tests, CPU)
+int sb_debug_alloc(uint64_t bytes) {
+    return guarded([&]() {
+        void* p = nullptr;
+        dev_malloc(&p, (size_t)bytes, "sb_debug_alloc");
+        SB_HIP(hipFree(p));
+        return SB_OK;
+    });
+}
 #ifndef SB_BUILD_ID
 #define SB_BUILD_ID "unknown"
 #endif
@@ -1487,7 +1532,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         const bool distm = cfg->world_size > 1 || (cfg->flags & 2);   // bit 1: sharded protocol at any world size
         const uint64_t tcap = distm ? 1024 : cap;   // sharded: the trail lives in the owner shards (E.own)
         E.tab_mask = tcap - 1;
-        SB_HIP(hipMalloc((void**)&E.tab, tcap * sizeof(Entry)));
+        dev_malloc((void**)&E.tab, tcap * sizeof(Entry), "visited set");
         SB_HIP(hipMemsetAsync(E.tab, 0xFF, tcap * sizeof(Entry), E.s));
         if (distm) {
             if (cfg->rank < 0 || cfg->rank >= cfg->world_size || cfg->world_size > 64)
@@ -1495,7 +1540,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
             E.own_mask = cap - 1;
             E.mig = (cfg->flags & 256) != 0 && cfg->world_size > 1;   // card-set ownership (sb_mig.inc)
             E.oe = E.mig && (cfg->flags & 512) != 0;                    // owner emission (sb_oe.inc)
-            SB_HIP(hipMalloc((void**)&E.own, cap * sizeof(Entry)));
+            dev_malloc((void**)&E.own, cap * sizeof(Entry), "owner visited shard");
             SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
         }
         SB_HIP(hipMalloc((void**)&E.d_small, 272 * 4));

@@ -22,16 +22,24 @@ struct HipError {
                                          std::to_string(__LINE__)};                                         \
     } while (0)
 
+// ---- device allocation with a diagnosable failure: the message names what was being allocated, the bytes
+// requested and the HBM free at that moment (an OOM in one rank of eight sharing a GPU must be
+// readable from one run).  SB_DEBUG_HBM_LIMIT=<bytes> (tests) fails every single request above that size the same way.
+std::string oom_message(const char* what, size_t bytes, hipError_t code);
+void dev_malloc(void** p, size_t bytes, const char* what);
+
 // ---- device buffer helper (grow-only) ----
 template <class T>
 struct DBuf {
     T* p = nullptr;
     size_t cap = 0;
-    void ensure(size_t n) {
+    void ensure(size_t n, const char* what = "engine buffer") {
         if (n <= cap) return;
         if (p) SB_HIP(hipFree(p));
+        p = nullptr;
+        cap = 0;
         size_t c = n < 1024 ? 1024 : n + n / 2;   // slack: a growing size reallocates rarely
-        SB_HIP(hipMalloc((void**)&p, c * sizeof(T)));
+        dev_malloc((void**)&p, c * sizeof(T), what);
         cap = c;
     }
     void release() {
@@ -52,7 +60,7 @@ struct Arena {
         if (bytes <= left) return;
         const size_t b = bytes > block_bytes ? bytes : block_bytes;
         void* p = nullptr;
-        SB_HIP(hipMalloc(&p, b));
+        dev_malloc(&p, b, "turn arena block");
         blocks.push_back(p);
         cur = (char*)p;
         left = b;
@@ -62,7 +70,7 @@ struct Arena {
         if (bytes > left) {
             const size_t b = bytes > block_bytes ? bytes : block_bytes;
             void* p = nullptr;
-            SB_HIP(hipMalloc(&p, b));
+            dev_malloc(&p, b, "turn arena block");
             blocks.push_back(p);
             cur = (char*)p;
             left = b;

@@ -39,7 +39,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument('--device', help='GPU ordinal (default 0)', type=int, default=0)
     p.add_argument('--gpus', help='shard the speedrun beam over N GPUs, one process each (default 1); RCCL between '
                                   'the GPUs (its asynchronous exchanges are verified with a completion-contract test '
-                                  'double and gloo, not yet on a multi-GPU node: SB_DIST_BACKEND=gloo forces gloo)',
+                                  'double and gloo, not yet on a multi-GPU node: SB_DIST_BACKEND=gloo forces gloo).  The trail '
+                                  'is owned by key hash, bit-exact; SB_DIST_MIG=1 (card-set ownership, faster) is NOT '
+                                  'bit-exact by construction: two card sets with an equal 64-bit key are both kept',
                    type=int,
                    default=1)
     return p

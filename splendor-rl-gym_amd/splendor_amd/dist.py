@@ -607,10 +607,14 @@ class DistSolve:
                 self._mark(st, 'expand')
             from_src = M[:, me]                               # records each source sends me in this part
             if ans_base + int(from_src.sum()) > cap:
-                # the receive bound is an estimate (max raw ratio so far + 50%), not a worst case
-                raise RuntimeError(f'sharded dedup: {ans_base + int(from_src.sum())} records received this turn '
-                                   f'exceed the receive bound {cap} estimated from the raw ratio so far '
-                                   '(sbd_expand_parts lostb_cap): capacity estimate exceeded, not out of memory')
+                # the receive bound is an estimate (max raw ratio so far + 50%), not a worst case; the exact count
+                # is known here, before the part's claims: grow the lost bits / tags and the answer buffer
+                cap = b.grow_receive(ans_base + int(from_src.sum()))
+                with ctx():
+                    grown = b.answer_buffer(cap)
+                    if ans_base:
+                        grown[:ans_base].copy_(ret[:ans_base])
+                ret = grown
             ostart = np.concatenate([[0], np.cumsum(cnt)])
             with ctx():
                 key = b.part_pack(j, int(ostart[-1]), send_base)
@@ -867,8 +871,14 @@ class HipBackend:
 
     # world > 1: the key pass (flags bit 6, sb_keypass.inc) instead of the expansion kernel + owner partition
     KEYPASS = os.environ.get('SB_DIST_KEYPASS', '1') != '0'
-    # world > 1: card-set ownership of the trail (flags bit 8, sb_mig.inc) instead of key ownership
+    # world > 1: card-set ownership of the trail (flags bit 8, sb_mig.inc) instead of key ownership.  NOT bit-exact
+    # by construction: the reference's equality is the 64-bit key (src/solver.py:332-336), and two states of
+    # different card sets with an equal key are claimed on two owners and both kept (≈0.06 such pairs expected
+    # per C5 solve, none in any golden).  Opt-in only; every surface that enables it says so (MIG_CAVEAT).
     MIG = os.environ.get('SB_DIST_MIG', '0') == '1'
+    MIG_CAVEAT = ('card-set ownership of the trail (SB_DIST_MIG=1 / flags bit 8) is not bit-exact by construction: '
+                  'two states of different card sets with an equal 64-bit key are both kept, where the reference '
+                  '(hash equality, src/solver.py:332-336) keeps the first')
     # with card-set ownership: owner emission (flags bit 9, sb_oe.inc), survivors emitted on the expanding ranks
     OE = os.environ.get('SB_DIST_OE', '0') == '1'
     PARTS = int(os.environ.get('SB_DIST_PARTS', '4'))   # exchange parts of the pipelined key pass (<= 16)
@@ -886,11 +896,14 @@ class HipBackend:
         torch.cuda.set_device(self.device)
         self.mig = bool(self.MIG or (int(extra_flags) & 256)) and world > 1
         self.oe = self.mig and bool(self.OE or (int(extra_flags) & 512))
+        if self.mig and rank == 0:
+            import warnings
+            warnings.warn(self.MIG_CAVEAT, stacklevel=2)
         self.timing = bool(int(extra_flags) & 1)   # key-pass device time per step (sbd_keypass_ms)
         self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 177) | (64 if self.KEYPASS and world > 1 else 0) |
+                         flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and world > 1 else 0) |
                          (256 if self.mig else 0) | (512 if self.oe else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
@@ -923,6 +936,7 @@ class HipBackend:
         lib.sbd_part_pack.argtypes = [vp, i32, vp, i64]
         lib.sbd_set_claim_stream.argtypes = [vp, vp]
         lib.sbd_owner_total.argtypes = [vp, i64]
+        lib.sbd_grow_receive.argtypes = [vp, i64, p64]
         lib.sbd_expand_defer.argtypes = [vp]
         lib.sbd_raw_total.argtypes = [vp, p64]
         lib.sbd_pack.argtypes = [vp, vp, vp]
@@ -1055,6 +1069,13 @@ class HipBackend:
             key = self._empty(max(int(n), 1))[:int(n)]
         self._chk(self.lib.sbd_part_pack(self.h, int(j), key.data_ptr() if n else None, int(send_base)), 'sbd_part_pack')
         return key
+
+    def grow_receive(self, n_needed) -> int:
+        """The turn's receive bound raised to >= n_needed (sbd_grow_receive: drains this rank's streams, keeps the
+        lost bits / tags so far); returns the new bound."""
+        cap = self.C.c_int64()
+        self._chk(self.lib.sbd_grow_receive(self.h, int(n_needed), self.C.byref(cap)), 'sbd_grow_receive')
+        return cap.value
 
     def owner_total(self, n):
         self._chk(self.lib.sbd_owner_total(self.h, int(n)), 'sbd_owner_total')

@@ -51,6 +51,8 @@ def _worker(rank, world, port, cfg, outdir):
         b.mig, b.force0 = True, cfg.get('force0', False)
         b.oe = cfg.get('oe', False)   # owner emission: survivors emitted on the expanding ranks
         b.parts = b.parts or 2
+    if cfg.get('small_cap'):   # a receive bound far below the records received: the host grows it (sbd_grow_receive)
+        b.recv_cap = cfg['small_cap']
     if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
         from deferred_comm import DeferredComm
         comm = DeferredComm(torch.device('cpu'))
@@ -72,7 +74,8 @@ def _worker(rank, world, port, cfg, outdir):
     out = {'trace': trace, 'counts': [c.tolist() for c in solve.counts], 'path': [list(x) for x in solve.path()],
            'slices': [[lo, hi, par] for lo, hi, par in b.turns],
            'mt': b.mt_state().tolist() if cfg['heur'] else None,
-           'deferred': [comm.deferred_calls, comm.waits] if cfg.get('deferred') else None}
+           'deferred': [comm.deferred_calls, comm.waits] if cfg.get('deferred') else None,
+           'grown': getattr(b, 'grown', 0)}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     dist.destroy_process_group()
@@ -140,6 +143,11 @@ CASES = [
          'oe': True}),
     (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'mig': True, 'force0': True,
          'oe': True}),
+    # the receive bound (an estimate) exceeded mid-turn: grown from the exact counts instead of failing
+    (3, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'small_cap': 8}),
+    (2, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'parts': 2, 'small_cap': 8,
+         'deferred': True}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'mig': True, 'small_cap': 8}),
 ]
 
 
@@ -170,6 +178,8 @@ def test_sharded_solve_matches_oracle(world, cfg):
     assert all([tuple(p) for p in r['path']] == path for r in res)
     if cfg['heur']:
         assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    if cfg.get('small_cap'):
+        assert any(r['grown'] for r in res), 'no rank grew its receive bound'
     if cfg.get('deferred'):   # the deferred path really ran: every rank issued async exchanges and waited for each
         assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), [r['deferred'] for r in res]
     o.close()

@@ -51,18 +51,25 @@ def test_realistic_c4_w1m_oracle_golden():
     eng.close()
 
 
-def _wait_device_memory(min_free_gib=240.0, timeout_s=120.0):
+def _wait_device_memory(min_free_gib=240.0, timeout_s=120.0, mem_get_info=None):
     """Wait until the device has released a previous multi-process test's memory (eight ranks of C5 need most
-    of the 288 GB; the exited ranks' allocations are reclaimed asynchronously)."""
+    of the 288 GB; the exited ranks' allocations are reclaimed asynchronously).  Fails the test (a precondition,
+    not a protocol result) with the free and needed HBM when it does not come back in time."""
     import time
-
-    import torch
+    if mem_get_info is None:
+        import torch
+        mem_get_info = lambda: torch.cuda.mem_get_info(0)
     t0 = time.time()
-    while time.time() - t0 < timeout_s:
-        free, _ = torch.cuda.mem_get_info(0)
+    free = 0
+    while True:
+        free, _ = mem_get_info()
         if free >= min_free_gib * 2**30:
-            return
-        time.sleep(2.0)
+            return free
+        if time.time() - t0 >= timeout_s:
+            break
+        time.sleep(min(2.0, timeout_s / 4))
+    pytest.fail(f'device memory not released in {timeout_s:.0f} s: {free / 2**30:.1f} GiB free, '
+                f'{min_free_gib:.1f} GiB needed (a previous test\'s ranks still hold HBM; not a protocol failure)')
 
 
 def _free_port():
@@ -85,7 +92,7 @@ def _digest_turn(outdir, t, world):
 def _worker(rank, world, port, cfg, outdir):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd')):
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'), here):
         if p not in sys.path:
             sys.path.insert(0, p)
     import torch.distributed as dist
@@ -106,11 +113,18 @@ def _worker(rank, world, port, cfg, outdir):
                    heuristic=HEURISTIC_IDS[cfg['heuristic']], beam_width=cfg['width'],
                    mt_state625=random.getstate()[1], visited_log2=cfg.get('visited_log2', 0),
                    extra_flags=cfg.get('flags', 0))
-    solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=True, beam_width=cfg['width'])
+    if cfg.get('devdeferred'):   # Comm's RCCL branches under RCCL's device-side completion contract
+        from device_deferred_comm import DeviceDeferredComm
+        comm = DeviceDeferredComm(b.device)
+    else:
+        comm = Comm(b.device)
+    solve = DistSolve(b, comm, goal_pts=cfg['goal'], use_heuristic=True, beam_width=cfg['width'])
     trace = []
     while True:
         st = solve.step()
         trace.append(st)
+        if cfg.get('devdeferred'):
+            comm.check_step()
         if st['done']:
             break
         np.save(os.path.join(outdir, f'keys_t{len(trace)}_r{rank}.npy'), b.turn_keys(len(trace)))
@@ -122,7 +136,8 @@ def _worker(rank, world, port, cfg, outdir):
                       flush=True)   # progress (pytest -s) for long runs
             dist.barrier()
     out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist(),
-           'visited_capacity': list(b.visited_capacity())}
+           'visited_capacity': list(b.visited_capacity()),
+           'deferred': [comm.deferred_calls, comm.waits, comm.landings] if cfg.get('devdeferred') else None}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     b.close()
@@ -132,14 +147,20 @@ def _worker(rank, world, port, cfg, outdir):
 @pytest.mark.parametrize('world,name,backend,flags', [(1, 'oracle_g15_balanced_w4000000_s0.json', 'gloo', 0),
                                                       (1, 'oracle_g15_balanced_w4000000_s0.json', 'nccl', 0),
                                                       (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo', 0),
-                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo', 256)])
+                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'gloo', 256),
+                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'devdeferred', 0),
+                                                      (2, 'oracle_g15_efficiency_w4000000_s0.json', 'devdeferred', 768)])
 def test_sharded_w4m_oracle_golden(world, name, backend, flags):
     """The sharded protocol at W=4M.  The nccl case is the C3 solve as `bench.py --gpus 1` with SB_FORCE_DIST=1
     runs it: init_process_group('nccl', device_id=...), the engine on torch's stream (sbd_set_stream) and
-    Comm's RCCL branches (a world of one: RCCL refuses two ranks on one GPU)."""
+    Comm's RCCL branches (a world of one: RCCL refuses two ranks on one GPU).  The devdeferred cases run Comm's RCCL
+    branches at world 2 under RCCL's device-side completion contract (tests/device_deferred_comm.py, gloo moving
+    the data): the key-owner pipelined protocol and card-set ownership + owner emission (flags 768)."""
     g = golden(name)
+    devdeferred = backend == 'devdeferred'
     cfg = {'goal': g['goal'], 'heuristic': g['heuristic'], 'width': g['beam_width'], 'seed': g['seed'],
-           'backend': backend, 'flags': flags}   # flags 256: card-set ownership of the trail (sb_mig.inc)
+           'backend': 'gloo' if devdeferred else backend, 'flags': flags,   # flags 256: card-set ownership (sb_mig.inc)
+           'devdeferred': devdeferred}
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         res = [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
@@ -154,6 +175,9 @@ def test_sharded_w4m_oracle_golden(world, name, backend, flags):
     path = [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in res[0]['path']]
     assert path == [p[5] for p in g['path']]
     assert all(oracle_c.mt_fingerprint(r['mt']) == g['final_mt'] for r in res)
+    if devdeferred:   # the async exchanges ran and each was waited for
+        assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), \
+            [r['deferred'] for r in res]
 
 
 C5 = 'oracle_g15_efficiency_w32000000_s0.json'

@@ -54,15 +54,25 @@ def _worker(rank, world, port, cfg, outdir):
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                    heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st, visited_log2=cfg.get('vlog2', 0),
                    extra_flags=cfg.get('flags', 0))
-    solve = DistSolve(b, Comm(b.device), goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
-    trace = solve.run()
+    if cfg.get('devdeferred'):   # Comm's RCCL branches under RCCL's device-side completion contract
+        from device_deferred_comm import DeviceDeferredComm
+        comm = DeviceDeferredComm(b.device)
+    else:
+        comm = Comm(b.device)
+    solve = DistSolve(b, comm, goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
+    trace = []
+    while not solve.done:
+        trace.append(solve.step())
+        if cfg.get('devdeferred'):
+            comm.check_step()
     slices = []
     for t in range(len(solve.counts)):
         n = int(solve.counts[t][rank])
         rows = [b.turn_state(t, r) for r in range(n)]
         slices.append([[x[0] for x in rows], [x[1] for x in rows], [x[2] for x in rows]])
     out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'slices': slices,
-           'mt': b.mt_state().tolist(), 'visited': list(b.visited_capacity())}
+           'mt': b.mt_state().tolist(), 'visited': list(b.visited_capacity()),
+           'deferred': [comm.deferred_calls, comm.waits, comm.landings] if cfg.get('devdeferred') else None}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     b.close()
@@ -113,6 +123,23 @@ CASES = [
     (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'ck': 1, 'flags': 768,
          'parts': 1}),
     (3, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 5000, 'seed': 12, 'heur': True, 'flags': 896}),
+    # the receive bound starts at 1024 records (flags bit 10): every turn past it grows the lost bits / tags and the
+    # answer buffer from the exact counts, mid-turn, with earlier parts' claims kept (sbd_grow_receive)
+    (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'flags': 1024, 'parts': 4}),
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 1024 | 256}),
+    # Comm's RCCL branches against the engine's two streams, under RCCL's device-side completion contract
+    # (tests/device_deferred_comm.py: receive buffers poisoned and filled late on a side stream, consumers ordered
+    # only by the waits the protocol makes, send pieces checked unchanged until completion): key ownership
+    # pipelined in 4 parts, card-set ownership + owner emission, the legacy chunked exchange, pure BFS
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'devdeferred': True}),
+    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'devdeferred': True}),
+    (4, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 768,
+         'devdeferred': True}),
+    (2, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'flags': 768,
+         'devdeferred': True}),
+    (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3, 'keypass': 0,
+         'devdeferred': True}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'devdeferred': True}),
 ]
 
 
@@ -139,6 +166,11 @@ def test_sharded_engine_matches_oracle(world, cfg):
     assert [tuple(p) for p in res[0]['path']] == o.path()
     if cfg['heur']:
         assert all(r['mt'] == o.mt_state().tolist() for r in res)
+    if cfg.get('devdeferred'):   # the RCCL branches really ran: async exchanges issued and each waited for
+        assert all(r['deferred'][2] > 0 for r in res), [r['deferred'] for r in res]
+        if world > 1 and cfg.get('keypass', 1):
+            assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), \
+                [r['deferred'] for r in res]
     if 'vlog2' in cfg:
         assert all(r['visited'][1] >= 2 and r['visited'][0] > (1 << cfg['vlog2']) for r in res), res[0]['visited']
     o.close()
