@@ -69,7 +69,10 @@ typedef struct {
                                   send no records; results unchanged); bit 8: card-set ownership of the
                                   sharded trail (sbd_mig_*, world_size > 1); bit 9 (with bit 8): owner
                                   emission (sbd_oe_*); bit 10 (test): the pipelined turn's receive bound starts at
-                                  1024 records, so the host grows it (sbd_grow_receive) every turn */
+                                  1024 records, so the host grows it (sbd_grow_receive) every turn; bit 11
+                                  (world_size > 1, key ownership): global-order claims — the own children become
+                                  records to this rank and every record of the turn is claimed in one pass in
+                                  global order (sbd_owner_claim_all) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -254,6 +257,13 @@ int sbd_owner_begin(sb_engine* e, int64_t n_total, int32_t nsrc, const int64_t* 
 int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, int64_t n, int32_t nseg, const int64_t* seg_start,
                     const int64_t* seg_base, uint8_t* d_ret);
 int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
+/* global-order claims (flags bit 11): after every part has arrived, the turn's n_total records in one pass, in
+ * virtual (source rank, part, record) order — the global (parent rank, ordinal) order; segment k = virtual records
+ * [v_start[k], v_start[k+1]) (the last to n_total) found at d_key + p_start[k].  d_ret[v] = 1 for a first occurrence,
+ * final after sbd_owner_finish.  The own children are records to this rank itself (sbd_part_counts / sbd_part_pack
+ * include them). */
+int sbd_owner_claim_all(sb_engine* e, const uint64_t* d_key, int64_t n_total, int32_t nseg, const int64_t* v_start,
+                        const int64_t* p_start, uint8_t* d_ret);
 /* answers over the wire as bits: dst[i] = bit k set iff src[8i + k] != 0 (n bytes -> ceil(n/8));
  * unpack is the inverse (n answer bytes from ceil(n/8) packed bytes).  Both on the engine stream. */
 int sbd_pack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);

@@ -20,7 +20,7 @@ PHASES = [
     ('expand', r'^k_expand<true>|^k_keys_a|^k_mkeys_a|^k_ks_counts|^k_raw_count|^k_scan_(tiles|reduce|apply)$'),
     ('record pack', r'^k_keys_b|^k_mkeys_b'),
     ('owner partition', r'^k_part_|^k_chunk_counts'),
-    ('owner claims', r'^k_own_|^k_mig_map|^k_mig_claim'),
+    ('owner claims', r'^k_own_|^k_mig_map|^k_mig_claim|^k_claim_goc'),
     ('answer bits', r'^k_(un)?pack_bits'),
     ('apply', r'^k_apply_w|^k_count_masks|^k_counts_i64|^k_total_i64'),
     ('noise (side stream)', r'^k_mt_'),

@@ -922,6 +922,9 @@ struct Engine {
     // its (owner, move, rank) word; per part its (owner, chunk) table + scan, per-owner counts (pinned mirror),
     // an event; received records' claims run on s_claim (sbd_set_claim_stream) beside the later parts
     bool ks_pipe = false;                 // this turn's expansion is the pipelined key pass
+    bool goc = false;                     // global-order claims (cfg flags bit 11, sb_dist.inc k_claim_goc)
+    DBuf<uint64_t> goc_seg;               // their segment table (v start, physical start)
+    uint64_t* h_goc = nullptr;            // pinned staging of it
     int ks_parts = 0;
     int64_t ks_c[17] = {};
     size_t ks_ccoff[17] = {};
@@ -1540,6 +1543,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
             E.own_mask = cap - 1;
             E.mig = (cfg->flags & 256) != 0 && cfg->world_size > 1;   // card-set ownership (sb_mig.inc)
             E.oe = E.mig && (cfg->flags & 512) != 0;                    // owner emission (sb_oe.inc)
+            E.goc = !E.mig && (cfg->flags & 2048) != 0;                 // global-order claims (key ownership)
             dev_malloc((void**)&E.own, cap * sizeof(Entry), "owner visited shard");
             SB_HIP(hipMemsetAsync(E.own, 0xFF, cap * sizeof(Entry), E.s));
         }
@@ -1869,6 +1873,8 @@ void sb_destroy(sb_engine* h) {
     for (auto& e : E.kp_ev)
         if (e) (void)hipEventDestroy(e);
     if (E.h_pc) (void)hipHostFree(E.h_pc);
+    if (E.h_goc) (void)hipHostFree(E.h_goc);
+    E.goc_seg.release();
     for (auto& e : E.ks_ev)
         if (e) (void)hipEventDestroy(e);
     if (E.d_tables) (void)hipFree(E.d_tables);

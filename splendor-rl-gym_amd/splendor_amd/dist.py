@@ -131,12 +131,14 @@ class Comm:
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
-    def alltoall_pieces(self, pieces, recv_sizes, what='other'):
+    def alltoall_pieces(self, pieces, recv_sizes, what='other', out=None):
         """Start an all_to_all of pieces[o] (views, any layout) to rank o; returns (receive buffer,
         handle).  RCCL runs it asynchronously on its own stream; wait(handle) orders this rank's stream
-        after it.  gloo (no list all_to_all) packs the pieces and completes at once."""
+        after it.  gloo (no list all_to_all) packs the pieces and completes at once.  out: a 1-D view to
+        receive into (sum(recv_sizes) elements), else a new buffer."""
         self.acct(what, self._remote(pieces))
-        out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=pieces[0].device)
+        if out is None:
+            out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=pieces[0].device)
         if self.cpu_coll:
             send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             r = torch.empty(int(sum(recv_sizes)), dtype=send.dtype)
@@ -575,11 +577,108 @@ class DistSolve:
         self._oe_noise_done = True
 
     def _dedup_parts(self, st, off):
-        back = self._exchange_parts(st)
+        back = self._exchange_parts_goc(st) if getattr(self.b, 'goc', False) else self._exchange_parts(st)
         all_n = self.c.gather_dev(self.b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
         self.b.apply_finish(int(all_n[self.c.rank]))
         self._mark(st, 'dedup_exchange')
         return self._post_dedup(st, all_n, off)
+
+    def _exchange_parts_goc(self, st):
+        """Dedup with the pipelined key pass and global-order claims (HipBackend.GOC, the default at world > 1 with
+        key ownership).  Every part's records — this rank's own children included, as records to itself — travel
+        as the parts complete (one all_to_all each, into one receive buffer, part-major), beside the later parts'
+        key pass; once all have arrived, one pass claims them in virtual (source, part, record) order, which is the
+        reference's (parent rank, ordinal) order (src/solver.py:446-450): first claims are then mostly the winners,
+        as on one GPU, instead of being displaced by records of earlier ranks that arrive later.  Tags: turn | v.
+        Then the answers go back as bits (per source and part, byte-aligned), one all_to_all."""
+        c, b = self.c, self.b
+        me, W, P = c.rank, c.world, b.parts
+        cs = b.claim_stream()
+        ctx = (lambda: torch.cuda.stream(cs)) if cs is not None else contextlib.nullcontext
+        sends, recvs, handles = [], [], []
+        send_base = ans_base = 0
+        ret = rbuf = None
+        cap = 0
+        for j in range(P):
+            cnt, cap_j = b.part_counts(j)                     # waits for part j's key pass only; self included
+            extra = [b.raw_total()] if j == 0 else []
+            M = c.allgather_array(np.concatenate([cnt, extra]), host=True)
+            if j == 0:
+                st['n_raw'] = int(M[:, W].sum())
+                M = M[:, :W]
+                cap = cap_j
+                b.owner_begin(cap, [0] * W)
+                with ctx():
+                    ret = b.answer_buffer(cap)
+                    rbuf = b.record_buffer(cap)
+                self._mark(st, 'expand')
+            from_src = M[:, me]                               # records each source (this rank too) sends me
+            need = ans_base + int(from_src.sum())
+            if need > cap:   # the receive bound is an estimate: grow it from the exact count, contents kept
+                cap = b.grow_receive(need)
+                with ctx():
+                    for hd in handles:                        # the earlier parts land before they are copied
+                        c.wait(hd)
+                    handles = []
+                    g_ret, g_rec = b.answer_buffer(cap), b.record_buffer(cap)
+                    if ans_base:
+                        g_rec[:ans_base].copy_(rbuf[:ans_base])
+                ret, rbuf = g_ret, g_rec
+            ostart = np.concatenate([[0], np.cumsum(cnt)])
+            with ctx():
+                key = b.part_pack(j, int(ostart[-1]), send_base)
+                pieces = [key[int(ostart[o]):int(ostart[o + 1])] for o in range(W)]
+                _, hd = c.alltoall_pieces(pieces, from_src, what='records', out=rbuf[ans_base:need])
+                handles.append(hd)
+            sends.append((cnt, send_base, ostart))
+            recvs.append((from_src, ans_base))
+            send_base += int(ostart[-1])
+            ans_base = need
+        # virtual order: source q's records, part by part; segment (q, j) at physical ans_base_j + sum(from_src_j[:q])
+        vst, pst, vseg = [], [], {}
+        v = 0
+        for q in range(W):
+            for j, (fs, ab) in enumerate(recvs):
+                vst.append(v)
+                pst.append(ab + int(fs[:q].sum()))
+                vseg[(q, j)] = v
+                v += int(fs[q])
+        b.owner_total(ans_base)
+        with ctx():
+            for hd in handles:
+                c.wait(hd)                                    # RCCL: the claim stream waits for every transfer
+            b.owner_claim_all(rbuf, ans_base, vst, pst, ret)
+            b.owner_finish(ret)
+        if cs is not None:
+            torch.cuda.current_stream().wait_stream(cs)
+        self._mark(st, 'a2a_keys+claim')
+        nb = lambda x: (int(x) + 7) // 8
+        sp = [0]
+        for q in range(W):
+            sp.append(sp[-1] + sum(nb(fs[q]) for fs, _ in recvs))
+        rp = [0]
+        for o in range(W):
+            rp.append(rp[-1] + sum(nb(cn[o]) for cn, _, _ in sends))
+        sbits = b.answer_buffer(sp[-1])
+        rbits = b.answer_buffer(rp[-1])
+        segs = []   # (answer offset, answers, bit-byte offset): every (source, part) segment in one launch
+        for q in range(W):
+            at = sp[q]
+            for j, (fs, _) in enumerate(recvs):
+                segs.append((vseg[(q, j)], int(fs[q]), at))
+                at += nb(fs[q])
+        b.pack_bits_segs(ret, segs, sbits)
+        c.alltoall_into([sbits[sp[q]:sp[q + 1]] for q in range(W)], [rbits[rp[o]:rp[o + 1]] for o in range(W)],
+                        what='answer bits')
+        back = b.answer_buffer(send_base)
+        segs = []
+        for o in range(W):
+            at = rp[o]
+            for cn, sb, os_ in sends:
+                segs.append((at, int(cn[o]), sb + int(os_[o])))
+                at += nb(cn[o])
+        b.unpack_bits_segs(rbits, segs, back)
+        return back
 
     def _exchange_parts(self, st, rec_words=1):
         """Dedup with the pipelined key pass (b.parts exchange parts of consecutive parents): for each part,
@@ -882,6 +981,9 @@ class HipBackend:
     # with card-set ownership: owner emission (flags bit 9, sb_oe.inc), survivors emitted on the expanding ranks
     OE = os.environ.get('SB_DIST_OE', '0') == '1'
     PARTS = int(os.environ.get('SB_DIST_PARTS', '4'))   # exchange parts of the pipelined key pass (<= 16)
+    # key ownership, world > 1: global-order claims (flags bit 11, sb_dist.inc k_claim_goc): own children become
+    # records to this rank and all records are claimed in one pass in global order once every part has arrived
+    GOC = os.environ.get('SB_DIST_GOC', '1') != '0'
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
                  heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0,
@@ -900,11 +1002,12 @@ class HipBackend:
             import warnings
             warnings.warn(self.MIG_CAVEAT, stacklevel=2)
         self.timing = bool(int(extra_flags) & 1)   # key-pass device time per step (sbd_keypass_ms)
+        self.goc = bool(self.GOC) and self.KEYPASS and world > 1 and not self.mig
         self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
                          flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and world > 1 else 0) |
-                         (256 if self.mig else 0) | (512 if self.oe else 0),
+                         (256 if self.mig else 0) | (512 if self.oe else 0) | (2048 if self.goc else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
         st = np.ascontiguousarray(np.array(mt_state625, dtype=np.uint32))
@@ -943,6 +1046,7 @@ class HipBackend:
         lib.sbd_owner_begin.argtypes = [vp, i64, i32, vp]
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_owner_finish.argtypes = [vp, vp]
+        lib.sbd_owner_claim_all.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_unpack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_pack_bits_segs.argtypes = [vp, vp, i32, vp, vp, vp, vp]
@@ -1123,6 +1227,17 @@ class HipBackend:
 
     def owner_finish(self, ret):
         self._chk(self.lib.sbd_owner_finish(self.h, ret.data_ptr()), 'sbd_owner_finish')
+
+    def record_buffer(self, n):
+        """The turn's receive buffer of record keys (global-order claims: every part lands in it)."""
+        return self._empty(max(int(n), 1))
+
+    def owner_claim_all(self, rbuf, n_total, v_start, p_start, ret):
+        vs = np.ascontiguousarray(v_start, dtype=np.int64)
+        ps = np.ascontiguousarray(p_start, dtype=np.int64)
+        self._chk(self.lib.sbd_owner_claim_all(self.h, rbuf.data_ptr() if n_total else None, int(n_total), len(vs),
+                                               vs.ctypes.data, ps.ctypes.data, ret.data_ptr() if n_total else None),
+                  'sbd_owner_claim_all')
 
     def pack_bits(self, src, dst):
         """dst (ceil(n/8) bytes) <- the n answer bytes of src as bits (bit k of byte i = src[8i + k])."""

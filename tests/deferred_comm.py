@@ -36,13 +36,15 @@ class DeferredComm(Comm):
         self.deferred_calls = 0
         self.waits = 0
 
-    def alltoall_pieces(self, pieces, recv_sizes, what='other'):
+    def alltoall_pieces(self, pieces, recv_sizes, what='other', out=None):
         self.acct(what, self._remote(pieces))
         snap = [p.clone() for p in pieces]
         send = torch.cat([p.reshape(-1) for p in snap]) if snap else torch.zeros(0)
         data = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype)
         dist.all_to_all_single(data, send, [int(x) for x in recv_sizes], [int(p.numel()) for p in pieces])
-        out = torch.full((int(sum(recv_sizes)),), _POISON[pieces[0].dtype], dtype=pieces[0].dtype)
+        if out is None:
+            out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype)
+        out.fill_(_POISON[pieces[0].dtype])
         h = _Deferred(out, data, list(pieces), snap)
         self.outstanding.append(h)
         self.deferred_calls += 1

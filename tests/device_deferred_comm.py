@@ -122,13 +122,14 @@ class DeviceDeferredComm(Comm):
         self._order(self._land([(out, r)]))
         return out
 
-    def alltoall_pieces(self, pieces, recv_sizes, what='other'):
+    def alltoall_pieces(self, pieces, recv_sizes, what='other', out=None):
         self.acct(what, self._remote(pieces))
         snap = [self._host(p) for p in pieces]
         send = torch.cat([x.reshape(-1) for x in snap])
         r = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype)
         dist.all_to_all_single(r, send, [int(x) for x in recv_sizes], [int(p.numel()) for p in pieces])
-        out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=self.device)
+        if out is None:
+            out = torch.empty(int(sum(recv_sizes)), dtype=pieces[0].dtype, device=self.device)
         guard = [(p, x.to(self.device)) for p, x in zip(pieces, snap)]
         h = _Handle(out, self._land([(out, r)], guard))
         self.outstanding.append(h)

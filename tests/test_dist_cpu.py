@@ -51,6 +51,8 @@ def _worker(rank, world, port, cfg, outdir):
         b.mig, b.force0 = True, cfg.get('force0', False)
         b.oe = cfg.get('oe', False)   # owner emission: survivors emitted on the expanding ranks
         b.parts = b.parts or 2
+    if cfg.get('goc'):   # global-order claims (HipBackend.GOC): own children as records, one claim pass
+        b.goc = True
     if cfg.get('small_cap'):   # a receive bound far below the records received: the host grows it (sbd_grow_receive)
         b.recv_cap = cfg['small_cap']
     if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
@@ -148,6 +150,19 @@ CASES = [
     (2, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 600, 'seed': 5, 'heur': True, 'parts': 2, 'small_cap': 8,
          'deferred': True}),
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'mig': True, 'small_cap': 8}),
+    # global-order claims: the own children become records to this rank, every record of the turn is claimed in one
+    # pass in (source, part, record) order once all parts arrived; answers by virtual index
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'goc': True}),
+    (3, {'goal': 5, 'hid': 0, 'name': 'simple', 'width': 97, 'seed': 2, 'heur': True, 'parts': 2, 'goc': True}),
+    (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'parts': 4, 'goc': True,
+         'deferred': True}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'parts': 2, 'goc': True,
+         'deferred': True}),
+    (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'parts': 2, 'goc': True}),
+    (3, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'goc': True,
+         'small_cap': 8, 'deferred': True}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'parts': 4,
+         'goc': True}),
 ]
 
 
