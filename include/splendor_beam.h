@@ -327,10 +327,13 @@ int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t wo
 /* kept records grouped by destination, next_queue order inside a group, one all_to_all buffer of at least the
  * kept count (the local next_queue size always suffices, so it can be enqueued before the counts reach the host).
  * 3 x u64 per record (state lo, state hi, global parent rank | noise draw << 32: the receiver re-scores it);
- * with owner emission (flags bit 9) the third word is global parent rank (25 bits) | draw << 25 | position << 32 */
-int sbd_pack_kept(sb_engine* e, uint64_t* d_rec);
-/* the new slice: n received 3-word records (global next_queue order, or with owner emission
- * source segments in position order), stable-sorted by score if heur */
+ * with owner emission (flags bit 9) the third word is global parent rank (25 bits) | draw << 25 | position << 32.
+ * rec20 != 0 (without owner emission; the caller's choice, the same on every rank, when every global parent rank of
+ * the turn is < 2^25): 20-byte records, five u32 (lo, hi, parent (25 bits) | draw << 25) — 17% fewer bytes on the
+ * rebalance's wire */
+int sbd_pack_kept(sb_engine* e, uint64_t* d_rec, int32_t rec20);
+/* the new slice: n received records in the form sbd_pack_kept wrote (global next_queue order, or with owner
+ * emission source segments in position order), stable-sorted by score if heur */
 int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);
 int sbd_mark_done(sb_engine* e, int64_t winner_rank_local);
 

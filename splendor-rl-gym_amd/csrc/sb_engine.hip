@@ -923,6 +923,7 @@ struct Engine {
     // an event; received records' claims run on s_claim (sbd_set_claim_stream) beside the later parts
     bool ks_pipe = false;                 // this turn's expansion is the pipelined key pass
     bool goc = false;                     // global-order claims (cfg flags bit 11, sb_dist.inc k_claim_goc)
+    bool kept20 = false;                  // this turn's kept records are 20 bytes (sbd_pack_kept rec20)
     DBuf<uint64_t> goc_seg;               // their segment table (v start, physical start)
     uint64_t* h_goc = nullptr;            // pinned staging of it
     int ks_parts = 0;

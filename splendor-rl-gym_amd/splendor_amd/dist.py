@@ -812,7 +812,8 @@ class DistSolve:
         else:
             dest_dev = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
-        rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank])   # enqueued ahead of the counts' round trip
+        # 20-byte kept records when every global parent rank of the turn fits 25 bits (the same choice on every rank)
+        rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank], rec20=st['n_parents'] <= (1 << 25))   # ahead of the counts
         if c.world == 1:   # every kept record stays: K of them, known here (no round trip)
             dest_counts = recv = np.array([K], dtype=np.int64)
         else:
@@ -1068,7 +1069,7 @@ class HipBackend:
         lib.sbd_noise_fill.argtypes = [vp, i32, vp, vp, u64, u64]
         lib.sbd_partition.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
-        lib.sbd_pack_kept.argtypes = [vp, vp]
+        lib.sbd_pack_kept.argtypes = [vp, vp, i32]
         lib.sbd_receive.argtypes = [vp, vp, i64, i32]
         lib.sbd_mark_done.argtypes = [vp, i64]
         lib.sbd_mig_launch.argtypes = [vp, i32]
@@ -1343,13 +1344,17 @@ class HipBackend:
                   'sbd_partition_bfs')
         return counts
 
-    def pack_kept(self, n_rows):
+    def pack_kept(self, n_rows, rec20=False):
         """Kept records grouped by destination into a buffer of n_rows (>= the kept count: the local
         next_queue size), enqueued before the counts reach the host."""
-        # 3 words (lo, hi, parent | draw << 32; with owner emission parent | draw << 25 | position << 32): the
-        # receiver re-scores them
-        rec = torch.empty((max(int(n_rows), 1), 3), dtype=torch.int64, device=self.device)
-        self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None), 'sbd_pack_kept')
+        # 3 words (lo, hi, parent | draw << 32; with owner emission parent | draw << 25 | position << 32), or with
+        # rec20 five u32 (lo, hi, parent | draw << 25): the receiver re-scores them
+        rec20 = bool(rec20) and not self.oe
+        if rec20:
+            rec = torch.empty((max(int(n_rows), 1), 5), dtype=torch.int32, device=self.device)
+        else:
+            rec = torch.empty((max(int(n_rows), 1), 3), dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_pack_kept(self.h, rec.data_ptr() if n_rows else None, int(rec20)), 'sbd_pack_kept')
         return rec
 
     # ---------------------------------------------------------------- card-set ownership (sb_mig.inc)
