@@ -157,6 +157,13 @@ def main():
             inst[name].append((t1 - t0) / 1e6)
     cap = {k: 1.5 * sorted(v)[len(v) // 2] for k, v in inst.items()}
     robust = [rank_table(allrows[r], a.steps, None, cap)[0] for r in range(a.world)]
+    # per kernel (robust: capped as above), ms per step, mean over ranks: what each phase is made of
+    perk = defaultdict(float)
+    for rows in allrows:
+        cut = 'k_mig_digit' if any(r[0] == 'k_mig_digit' for r in rows) else 'k_raw_count'
+        ex = [i for i, r in enumerate(rows) if r[0] == cut]
+        for name, t0, t1 in rows[ex[-a.steps]:]:
+            perk[name] += min((t1 - t0) / 1e6, cap.get(name, 1e30)) / a.steps / a.world
     keys = list(ranks[0].keys())
     mean = {k: sum(t[k] for t in ranks) / len(ranks) for k in keys}
     worst = {k: max(t[k] for t in ranks) for k in keys}
@@ -167,11 +174,13 @@ def main():
         print(f'{k:34s} {mean[k]:9.3f} {worst[k]:9.3f} {rmean[k]:9.3f} {rworst[k]:9.3f}')
     if unk:
         print('unclassified:', {k: round(v, 3) for k, v in unk.items()})
+    print('per kernel (robust ms per step, mean of ranks):',
+          ', '.join(f'{k} {v:.3f}' for k, v in sorted(perk.items(), key=lambda kv: -kv[1])[:24]))
     if a.out:
         with open(a.out, 'w') as f:
             json.dump({'world': a.world, 'steps': a.steps, 'mean_ms': mean, 'max_ms': worst, 'per_rank_ms': ranks,
                        'robust_mean_ms': rmean, 'robust_max_ms': rworst, 'robust_per_rank_ms': robust,
-                       'unclassified_ms': unk}, f, indent=1)
+                       'unclassified_ms': unk, 'robust_per_kernel_ms': dict(perk)}, f, indent=1)
 
 
 if __name__ == '__main__':
