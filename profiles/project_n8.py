@@ -8,8 +8,10 @@ rank's kernels alone on the device = its own GPU's device time) and a bench line
 Model per rank and step: device time (the table's engine-stream total; the noise side stream overlaps) plus
 the exchanges that sit on the critical path at an effective all_to_all rate B per GPU (xGMI: 7 links per
 MI355X; RCCL's all_to_all rate is unmeasured here — one GPU per box — so B is a parameter), plus a fixed
-latency per collective round.  The records travel in parts beside the key pass, so only their excess over
-the key pass counts; every other exchange counts in full.
+latency per collective round.  The records travel in P parts beside the key pass: part j leaves when its key pass
+is done, so what the claims wait for beyond the key pass is max(x / P, x - kp (P - 1) / P) for a transfer time x
+and key pass kp (round 5: the last part's transfer always counts — earlier rounds counted only max(0, x - kp)).
+Every other exchange counts in full.
     python3 profiles/project_n8.py TABLE.json BENCH.json [--B 250,400,600] [--lat-us 30] [--rounds 20]
 """
 import argparse
@@ -25,11 +27,12 @@ def main():
     ap.add_argument('--B', default='250,400,600', help='effective all_to_all GB/s per GPU')
     ap.add_argument('--lat-us', type=float, default=30.0, help='latency per collective round (us)')
     ap.add_argument('--rounds', type=int, default=20, help='collective rounds per step on the critical path')
-    ap.add_argument('--single-ms', type=float, default=4.703, help='one GPU ms/step (BENCH_r03: 4.703)')
+    ap.add_argument('--single-ms', type=float, default=4.548, help='one GPU ms/step (BENCH_r04: 4.548)')
     ap.add_argument('--balanced-kept', action='store_true',
                     help='kept records as if every rank sent 7/8 of W x 32 B (a protocol whose kept records are produced '
                          'evenly); by default rank 0, which sends the most, as measured')
     ap.add_argument('--W', type=float, default=4e6, help='parents per rank')
+    ap.add_argument('--parts', type=int, default=4, help='exchange parts of the key pass (SB_DIST_PARTS)')
     a = ap.parse_args()
     t = json.load(open(a.table))
     b = [json.loads(l) for l in open(a.bench) if l.startswith('{')][-1]
@@ -45,7 +48,8 @@ def main():
     for B in [float(v) for v in a.B.split(',')]:
         crit = sum(v for k, v in x.items() if k not in OVERLAPPED) / B          # MB / (GB/s) = ms
         over = sum(v for k, v in x.items() if k in OVERLAPPED) / B
-        exposed_rec = max(0.0, over - keypass)
+        P = a.parts
+        exposed_rec = max(over / P, over - keypass * (P - 1) / P) if over > 0 else 0.0
         lat = a.rounds * a.lat_us / 1e3
         step = dev + crit + exposed_rec + lat
         gps = 8 * a.W / (step * 1e-3) / 1e9

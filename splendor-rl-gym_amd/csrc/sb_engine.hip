@@ -97,6 +97,15 @@ constexpr int MAX_PROBE = 4096;
 // losing CAS attempts store here (see probe_insert); spread over 256 lines so they do not serialise
 __device__ unsigned long long g_claim_sink[4096];
 
+// hash(gems) of every 15-bit gem field (5 x 3 bits), 256 KB, L2-resident: the sharded key passes (VALU-bound: nothing
+// to hide the hashing under, unlike k_expand's probes) look a child's gem hash up instead of folding five lanes
+__device__ uint64_t g_hgems[1 << 15];
+__global__ void k_init_hgems() {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (1 << 15)) g_hgems[i] = hash_gems((uint32_t)i);
+}
+__device__ __forceinline__ uint64_t hash_gems_t(uint32_t gf) { return g_hgems[gf & 0x7FFFu]; }
+
 // Probe loads of the visited set.  -DSB_PROBE_NT=1 makes them non-temporal (global_load_dwordx4 ... nt):
 // alone, a random 16-B nt probe of a 32 GiB table runs at the cache-resident rate (54 G/s against 48 G/s,
 // profiles/micro/r2_randaccess2.txt), but inside k_expand it is 33% slower (expand 3.42 -> 4.56 ms,
@@ -189,8 +198,10 @@ constexpr int SH_Q_SHIFT = 34;
 constexpr uint64_t SH_LOCAL_MASK = (1ull << SH_Q_SHIFT) - 1;
 constexpr uint64_t SH_RANK_MASK = (1ull << (SH_Q_SHIFT - 8)) - 1;   // local parent ranks < 2^26
 
+// the top 24 bits of the key's mix scaled to [0, world) (multiply-shift, not a 64-bit modulo: a division routine
+// per child in the key pass)
 __host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
-    return (uint32_t)((mix64(key) >> 40) % world);
+    return (uint32_t)(((mix64(key) >> 40) * (uint64_t)world) >> 24);
 }
 
 template <bool PRE, bool SH = false>
@@ -929,6 +940,9 @@ struct Engine {
     int ks_parts = 0;
     int64_t ks_c[17] = {};
     size_t ks_ccoff[17] = {};
+    uint64_t ks_sbase[17] = {};           // each part's first index in the turn's send buffers (sbd_part_pack)
+    struct KpTab* h_kt = nullptr;         // pinned: the apply's answer-place table (global-order claims)
+    DBuf<uint64_t> d_kt;
     hipEvent_t ks_ev[16] = {};
     uint32_t* h_pc = nullptr;             // pinned: per part, per owner record counts (16 x 64)
     uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
@@ -1526,6 +1540,7 @@ int sb_create(const sb_config* cfg, const uint32_t* mt_state625, uint64_t root_l
         E.dev = cfg->device;
         SB_HIP(hipSetDevice(E.dev));
         create_streams(E.s, E.s_mt);
+        hipLaunchKernelGGL(k_init_hgems, dim3((1 << 15) / 256), dim3(256), 0, E.s);   // (per process and device: cheap)
         for (auto& e : E.ev) SB_HIP(hipEventCreate(&e));
         E.d_tables = upload_tables(E.s);
         int lg = cfg->visited_log2;
@@ -1875,6 +1890,8 @@ void sb_destroy(sb_engine* h) {
         if (e) (void)hipEventDestroy(e);
     if (E.h_pc) (void)hipHostFree(E.h_pc);
     if (E.h_goc) (void)hipHostFree(E.h_goc);
+    if (E.h_kt) (void)hipHostFree(E.h_kt);
+    E.d_kt.release();
     E.goc_seg.release();
     for (auto& e : E.ks_ev)
         if (e) (void)hipEventDestroy(e);
