@@ -16,3 +16,14 @@ pass sq2 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_S
 pass sq3 SQ_LEVEL_WAVES SQ_INSTS_FLAT SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_VMEM SQ_IFETCH || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $ARGS \
     > $O/trace.json 2> $O/trace.err || exit 1
+# A/B: the realistic expansion's gem / pool hashes from the table (default) against folded per child
+# (SB_RX2_NO_HTAB variant), two interleaved rounds of the C4 bench line
+V=$PWD/splendor-rl-gym_amd/splendor_amd/variants
+for R in 1 2; do
+    for L in default rxnotab; do
+        LIB=$PWD/splendor-rl-gym_amd/splendor_amd/libsplendor_beam.so; [ $L = rxnotab ] && LIB=$V/lib_rxnotab.so
+        SPLENDOR_BEAM_LIB=$LIB timeout -k 10 300 python3 bench.py --realistic --no-cpu-baseline --steps 12 --warmup 2 \
+            > $O/ab_${L}_$R.json 2> $O/ab_${L}_$R.err || exit 1
+        python3 -c "import json,sys; d=json.load(open('$O/ab_${L}_$R.json')); print('$L', $R, round(d['value']/1e6,1), d['ms_per_step'], d['phases_ms'])"
+    done
+done
