@@ -29,7 +29,8 @@ PKG_ROOT = os.path.join(os.path.dirname(HERE), 'splendor-rl-gym_amd')
 if PKG_ROOT not in sys.path:
     sys.path.insert(0, PKG_ROOT)
 
-from splendor_amd.deck import deck_rows  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))   # ref_tables beside this file
+from ref_tables import deck_rows  # noqa: E402  (the captured deck, not the product's deck.py)
 
 MAXG = 7
 _ROWS = list(deck_rows())   # 7 ints per card: cost[5], pt, colour

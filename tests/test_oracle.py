@@ -142,3 +142,21 @@ def test_oracle_prune_equals_stable_sort_slice(seed, n, W, vals):
     k = oracle_c.lib().oc_debug_prune(np.ascontiguousarray(key), n, W, out)
     ref = sorted(range(n), key=lambda i: int(key[i]), reverse=True)[:W]   # Python's stable sort, as the reference
     assert k == len(ref) and out[:k].tolist() == ref
+
+
+def test_oracle_tables_are_its_own():
+    """The checker does not share the product's tables: oracle_c / pyref take the deck from the
+    fixture captured by importing the reference and restate the state packing (oracle/ref_tables.py); the product's
+    deck.py must agree with that capture."""
+    import ast
+    import os
+
+    import ref_tables
+    from conftest import REPO
+    from splendor_amd.deck import deck_rows
+    for f in ('oracle_c.py', 'pyref.py', 'ref_tables.py'):
+        tree = ast.parse(open(os.path.join(REPO, 'oracle', f)).read())
+        mods = {n.module for n in ast.walk(tree) if isinstance(n, ast.ImportFrom) and n.module}
+        mods |= {a.name for n in ast.walk(tree) if isinstance(n, ast.Import) for a in n.names}
+        assert not any(m.startswith('splendor_amd') for m in mods), (f, mods)
+    assert ref_tables.deck_rows() == list(deck_rows())
