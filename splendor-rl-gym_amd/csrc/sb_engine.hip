@@ -910,6 +910,8 @@ struct Engine {
     DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
     DBuf<uint16_t> mrj;                   // card-set records: (parent in chunk << 8) | move, at the record's slot
     DBuf<uint8_t> snv;                    // sharded emission: each survivor's noise draw (3-word kept records)
+    DBuf<uint8_t> gdig, gcnt;             // grouped kept records: group starts by destination, their child counts
+    DBuf<uint32_t> gk_hist, gk_off, gk_cnt, gk_coff;   // ... group partition, buffer layout; receive: counts, offsets
     DBuf<uint64_t> rkey2;                 // owner emission: received records' re-scored keys, arrival order
     bool sdesc = false, sdesc32 = false;  // sharded emission wrote descriptors (4-byte when sdesc32) into nlo
     int64_t sdesc_goff = 0;               // ... global ranks: the slice's parents start at this one
@@ -1026,6 +1028,7 @@ static void check_err_word(Engine& E) {
     if (e & 32u) throw HipError{hipErrorLaunchFailure, "top-k sort fix-up: more distinct keys in one prefix run than it holds"};
     if (e & 64u) throw HipError{hipErrorOutOfMemory, "sharded records exceed the compact record buffers (flags bit 5)"};
     if (e & 128u) throw HipError{hipErrorLaunchFailure, "card-set sharded claims: a displaced record is not where its parent maps"};
+    if (e & 256u) throw HipError{hipErrorLaunchFailure, "grouped kept records: a segment's groups do not add up to its children"};
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -1877,6 +1880,12 @@ void sb_destroy(sb_engine* h) {
     E.xsurv.release();
     E.xsoff.release();
     E.kpos.release();
+    E.gdig.release();
+    E.gcnt.release();
+    E.gk_hist.release();
+    E.gk_off.release();
+    E.gk_cnt.release();
+    E.gk_coff.release();
     E.tpos.release();
     E.rowcnt.release();
     E.rownb.release();

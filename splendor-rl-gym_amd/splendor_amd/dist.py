@@ -44,6 +44,9 @@ NONE32 = 0xFFFFFFFF
 BIG = (1 << 62)
 
 
+# grouped kept records on the rebalance's wire (key ownership, world > 1): SB_DIST_GKR=0 sends the 20-byte records
+GKR = os.environ.get('SB_DIST_GKR', '1') != '0'
+
 class Comm:
     """torch.distributed helpers; gloo works on CPU tensors (device tensors are staged)."""
 
@@ -111,11 +114,11 @@ class Comm:
         if self.world == 1:
             c = counts.cpu().numpy()
             return c, c
-        send = self._to(counts)
+        send = self._to(counts.reshape(-1))   # world x k counts: k per destination (equal splits)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send)
         both = torch.cat([send, recv]).cpu().numpy()
-        return both[:self.world], both[self.world:]
+        return both[:send.numel()], both[send.numel():]
 
     def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
         send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
@@ -812,8 +815,53 @@ class DistSolve:
         else:
             dest_dev = b.partition_bfs(k_off, N, G)
         self._mark(st, 'select')
-        # 20-byte kept records when every global parent rank of the turn fits 25 bits (the same choice on every rank)
-        rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank], rec20=st['n_parents'] <= (1 << 25))   # ahead of the counts
+        # 20-byte kept records when every global parent rank of the turn fits 25 bits (the same choice on every rank);
+        # world > 1 with key ownership: grouped by (parent, destination) on the wire (sbd_pack_kept_grouped)
+        rec20 = st['n_parents'] <= (1 << 25)
+        if GKR and c.world > 1 and rec20 and not oe and not self.mig and hasattr(b, 'pack_kept_grouped'):
+            self._rebalance_grouped(st, all_n)
+        else:
+            self._rebalance(st, all_n, K, dest_dev, oe, rec20)
+        if self.heur:
+            self.noise.background()
+        if self.lookahead:
+            self._launch_front(K)   # the next turn's expansion (K parents in all) overlaps its goal check
+        else:   # a benchmark's window edge (bench.py): the next step() launches it
+            self._front_deferred = True
+        self._turn_sync()
+        self._mark(st, 'rebalance')
+        st['xbytes'] = dict(c.xbytes)
+        self.turn += 1
+        st['n_kept'] = int(self.counts[-1].sum())
+        return st
+
+    def _rebalance_grouped(self, st, all_n):
+        """kept records to their destination ranges as (parent, destination) groups: one count exchange of
+        (children, groups) pairs, one all_to_all of the segments (5 G + ceil(C / 2) u32 each; this rank's own
+        copied), the receiver expands them into the 20-byte records, then receives them as usual."""
+        c, b = self.c, self.b
+        buf, cnt2 = b.pack_kept_grouped(all_n[c.rank])   # ahead of the counts
+        send2, recv2 = c.alltoall_counts_dev(cnt2)
+        send2 = np.asarray(send2, dtype=np.int64).reshape(c.world, 2)
+        recv2 = np.asarray(recv2, dtype=np.int64).reshape(c.world, 2)
+        ssz = 5 * send2[:, 1] + (send2[:, 0] + 1) // 2
+        rsz = 5 * recv2[:, 1] + (recv2[:, 0] + 1) // 2
+        self._mark(st, 'pack_kept')
+        me = c.rank
+        so = np.concatenate([[0], np.cumsum(ssz)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(rsz)]).astype(np.int64)
+        rbuf = torch.empty(max(int(ro[-1]), 1), dtype=torch.int32, device=buf.device)
+        pieces = [buf[int(so[q]):int(so[q + 1])] if q != me else buf[:0] for q in range(c.world)]
+        outs = [rbuf[int(ro[q]):int(ro[q + 1])] if q != me else rbuf[:0] for q in range(c.world)]
+        c.alltoall_into(pieces, outs, what='kept records')
+        rbuf[int(ro[me]):int(ro[me + 1])].copy_(buf[int(so[me]):int(so[me + 1])])
+        self._mark(st, 'a2a_kept')
+        rrec = b.unpack_kept(rbuf, ro[:-1], recv2[:, 1], recv2[:, 0])
+        b.receive(rrec, self.heur)
+
+    def _rebalance(self, st, all_n, K, dest_dev, oe, rec20):
+        c, b = self.c, self.b
+        rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank], rec20=rec20)   # ahead of the counts
         if c.world == 1:   # every kept record stays: K of them, known here (no round trip)
             dest_counts = recv = np.array([K], dtype=np.int64)
         else:
@@ -835,18 +883,6 @@ class DistSolve:
         if oe:   # each source's records in position order: the receive merges them
             b.oe_segments(ro)
         b.receive(rrec, self.heur)
-        if self.heur:
-            self.noise.background()
-        if self.lookahead:
-            self._launch_front(K)   # the next turn's expansion (K parents in all) overlaps its goal check
-        else:   # a benchmark's window edge (bench.py): the next step() launches it
-            self._front_deferred = True
-        self._turn_sync()
-        self._mark(st, 'rebalance')
-        st['xbytes'] = dict(c.xbytes)
-        self.turn += 1
-        st['n_kept'] = int(self.counts[-1].sum())
-        return st
 
     SEL_PASSES = 7   # ceil(64 / 10): passes after the last digit are no-ops on the device
 
@@ -1007,7 +1043,7 @@ class HipBackend:
         self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and world > 1 else 0) |
+                         flags=2 | (int(extra_flags) & (1201 | 4096)) | (64 if self.KEYPASS and world > 1 else 0) |
                          (256 if self.mig else 0) | (512 if self.oe else 0) | (2048 if self.goc else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
@@ -1070,6 +1106,8 @@ class HipBackend:
         lib.sbd_partition.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
         lib.sbd_pack_kept.argtypes = [vp, vp, i32]
+        lib.sbd_pack_kept_grouped.argtypes = [vp, vp, i64, vp]
+        lib.sbd_unpack_kept.argtypes = [vp, vp, i32, p64, p64, p64, vp]
         lib.sbd_receive.argtypes = [vp, vp, i64, i32]
         lib.sbd_mark_done.argtypes = [vp, i64]
         lib.sbd_mig_launch.argtypes = [vp, i32]
@@ -1343,6 +1381,28 @@ class HipBackend:
         self._chk(self.lib.sbd_partition_bfs(self.h, int(k_off), int(N), int(G), counts.data_ptr()),
                   'sbd_partition_bfs')
         return counts
+
+    def pack_kept_grouped(self, n_rows):
+        """Grouped kept records (sbd_pack_kept_grouped): (int32 buffer of 22 bytes per local survivor, device
+        int64 (C_d, G_d) pairs per destination), enqueued before the counts reach the host."""
+        cap = 22 * int(n_rows) // 4 + 2 * self.world + 2
+        buf = torch.empty(max(cap, 1), dtype=torch.int32, device=self.device)
+        cnt2 = torch.zeros(2 * self.world, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_pack_kept_grouped(self.h, buf.data_ptr(), cap, cnt2.data_ptr()), 'sbd_pack_kept_grouped')
+        return buf, cnt2
+
+    def unpack_kept(self, rbuf, bases, groups, children):
+        """The received groups (source segments at u32 offsets bases, in source order) as (n, 5) int32 records."""
+        n = int(np.sum(children))
+        rec = torch.empty((max(n, 1), 5), dtype=torch.int32, device=self.device)
+        b = np.ascontiguousarray(bases, dtype=np.int64)
+        g = np.ascontiguousarray(groups, dtype=np.int64)
+        c = np.ascontiguousarray(children, dtype=np.int64)
+        P = self.C.POINTER(self.C.c_int64)
+        self._chk(self.lib.sbd_unpack_kept(self.h, rbuf.data_ptr() if rbuf.numel() else None, len(b),
+                                           b.ctypes.data_as(P), g.ctypes.data_as(P), c.ctypes.data_as(P),
+                                           rec.data_ptr()), 'sbd_unpack_kept')
+        return rec[:n]
 
     def pack_kept(self, n_rows, rec20=False):
         """Kept records grouped by destination into a buffer of n_rows (>= the kept count: the local

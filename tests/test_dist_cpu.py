@@ -27,6 +27,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, cfg, outdir):
+    if 'gkr' in cfg:   # grouped kept records on the rebalance's wire (dist.GKR, read at import)
+        os.environ['SB_DIST_GKR'] = '1' if cfg['gkr'] else '0'
     if 'chunks' in cfg:
         os.environ['SB_DIST_CHUNKS'] = str(cfg['chunks'])
         os.environ['SB_DIST_CHUNK_MIN'] = '0'
@@ -112,6 +114,9 @@ CASES = [
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'parts': 4}),
     (3, {'goal': 5, 'hid': 1, 'name': 'balanced', 'width': 200, 'seed': 4, 'heur': True, 'serialize': True,
          'parts': 2}),
+    # the 20-byte kept records instead of (parent, destination) groups on the rebalance's wire
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'gkr': False}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'parts': 4, 'gkr': False}),
     # Comm's RCCL branches under RCCL's completion contract (deferred receive buffers, poisoned until
     # wait): the pipelined protocol at worlds 2/4/8 and the chunked legacy exchange
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'deferred': True}),

@@ -35,6 +35,8 @@ def _worker(rank, world, port, cfg, outdir):
         os.environ['SB_NOISE_CK'] = str(cfg['ck'])
     if 'keypass' in cfg:   # 0: the expansion kernel + separate owner partition (sbd_expand_launch) at world > 1
         os.environ['SB_DIST_KEYPASS'] = str(cfg['keypass'])
+    if 'gkr' in cfg:       # grouped kept records on the rebalance's wire (default on)
+        os.environ['SB_DIST_GKR'] = '1' if cfg['gkr'] else '0'
     if 'parts' in cfg:     # exchange parts of the pipelined key pass (default 4)
         os.environ['SB_DIST_PARTS'] = str(cfg['parts'])
     import sys
@@ -127,6 +129,11 @@ CASES = [
     # answer buffer from the exact counts, mid-turn, with earlier parts' claims kept (sbd_grow_receive)
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'flags': 1024, 'parts': 4}),
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 1024 | 256}),
+    # kept records on the rebalance's wire: the 20-byte records instead of (parent, destination) groups; groups
+    # split every 3 children (flags bit 12), so rows of one parent follow each other in a segment
+    (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'gkr': False}),
+    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'flags': 4096}),
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 4096 | 128}),
     # Comm's RCCL branches against the engine's two streams, under RCCL's device-side completion contract
     # (tests/device_deferred_comm.py: receive buffers poisoned and filled late on a side stream, consumers ordered
     # only by the waits the protocol makes, send pieces checked unchanged until completion): key ownership
