@@ -72,8 +72,7 @@ typedef struct {
                                   1024 records, so the host grows it (sbd_grow_receive) every turn; bit 11
                                   (world_size > 1, key ownership): global-order claims — the own children become
                                   records to this rank and every record of the turn is claimed in one pass in
-                                  global order (sbd_owner_claim_all); bit 12 (test): grouped kept records hold
-                                  at most 3 children per row (sbd_pack_kept_grouped splits longer groups) */
+                                  global order (sbd_owner_claim_all) */
     /* multi-GPU (config 5): this engine owns global beam ranks [rank_lo, rank_hi) */
     int32_t world_size;        /* 1 for single-GPU */
     int32_t rank;
@@ -335,14 +334,14 @@ int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t wo
 int sbd_pack_kept(sb_engine* e, uint64_t* d_rec, int32_t rec20);
 /* grouped kept records (round 5; key ownership with descriptor emission, global parent ranks < 2^25): a source's
  * kept children of one parent bound for one destination travel as a group — a 20-byte row (parent lo, hi, global
- * rank (25 bits) | children (7 bits, <= 127)) and a u16 per child (move | draw << 8).  Destination d's segment of
+ * rank) and a u16 per child (move | draw << 8 | opens its group << 15).  Destination d's segment of
  * d_buf: its rows, then its child entries padded to 4 bytes (5 G_d + ceil(C_d / 2) u32).  cap_u32 >= 22 bytes per
  * local survivor / 4 (+ 2 world + 2).  d_counts2 (device, 2 x world int64): (C_d, G_d) pairs for the count exchange.
  * Replaces sbd_pack_kept(rec20) on the rebalance's wire; the receiver calls sbd_unpack_kept, then sbd_receive. */
 int sbd_pack_kept_grouped(sb_engine* e, uint32_t* d_buf, int64_t cap_u32, int64_t* d_counts2);
 /* receive side of the grouped records: nseg source segments of d_buf (host arrays: u32 base, groups, children of
  * each, in source order) expanded into the 20-byte records sbd_receive takes (d_rec: sum(children) x 5 u32, the
- * sources' segments concatenated in order).  Error word bit 256 if a segment's groups do not add up to its children. */
+ * sources' segments concatenated in order).  Error word bit 256 if a segment's group starts do not match its rows. */
 int sbd_unpack_kept(sb_engine* e, const uint32_t* d_buf, int32_t nseg, const int64_t* seg_base, const int64_t* seg_groups,
                     const int64_t* seg_children, uint32_t* d_rec);
 /* the new slice: n received records in the form sbd_pack_kept wrote (global next_queue order, or with owner

@@ -2,7 +2,7 @@
 # Round 5, session 9: grouped kept records on the rebalance's wire (sbd_pack_kept_grouped /
 # sbd_unpack_kept).  The sharded GPU tests (groups, the 20-byte form, 3-child split groups), the W=4M world-2 goldens,
 # then the serialised world-8 trace of the default build and its N=8 projection
-O=${1:-gpurun_out/r5s9}; mkdir -p $O
+O=${1:-gpurun_out/r5s10}; mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread > $O/dist.log 2>&1
 rc=$?; tail -1 $O/dist.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python3 -u -m pytest tests/test_gpu_big.py -x -v -k "w4m" --timeout 400 --timeout-method thread > $O/big.log 2>&1

@@ -910,8 +910,8 @@ struct Engine {
     DBuf<uint8_t> rdsc;                   // sharded: each record's move descriptor, at its raw position
     DBuf<uint16_t> mrj;                   // card-set records: (parent in chunk << 8) | move, at the record's slot
     DBuf<uint8_t> snv;                    // sharded emission: each survivor's noise draw (3-word kept records)
-    DBuf<uint8_t> gdig, gcnt;             // grouped kept records: group starts by destination, their child counts
-    DBuf<uint32_t> gk_hist, gk_off, gk_cnt, gk_coff;   // ... group partition, buffer layout; receive: counts, offsets
+    DBuf<uint8_t> gdig;                   // grouped kept records: group starts by destination
+    DBuf<uint32_t> gk_hist, gk_off, gk_cnt, gk_coff;   // ... group partition, buffer layout; receive: start flags, scan
     DBuf<uint64_t> rkey2;                 // owner emission: received records' re-scored keys, arrival order
     bool sdesc = false, sdesc32 = false;  // sharded emission wrote descriptors (4-byte when sdesc32) into nlo
     int64_t sdesc_goff = 0;               // ... global ranks: the slice's parents start at this one
@@ -1881,7 +1881,6 @@ void sb_destroy(sb_engine* h) {
     E.xsoff.release();
     E.kpos.release();
     E.gdig.release();
-    E.gcnt.release();
     E.gk_hist.release();
     E.gk_off.release();
     E.gk_cnt.release();

@@ -1043,7 +1043,7 @@ class HipBackend:
         self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & (1201 | 4096)) | (64 if self.KEYPASS and world > 1 else 0) |
+                         flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and world > 1 else 0) |
                          (256 if self.mig else 0) | (512 if self.oe else 0) | (2048 if self.goc else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()

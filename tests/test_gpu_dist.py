@@ -129,11 +129,8 @@ CASES = [
     # answer buffer from the exact counts, mid-turn, with earlier parts' claims kept (sbd_grow_receive)
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'flags': 1024, 'parts': 4}),
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 1024 | 256}),
-    # kept records on the rebalance's wire: the 20-byte records instead of (parent, destination) groups; groups
-    # split every 3 children (flags bit 12), so rows of one parent follow each other in a segment
+    # kept records on the rebalance's wire: the 20-byte records instead of (parent, destination) groups
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'gkr': False}),
-    (4, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'flags': 4096}),
-    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 4096 | 128}),
     # Comm's RCCL branches against the engine's two streams, under RCCL's device-side completion contract
     # (tests/device_deferred_comm.py: receive buffers poisoned and filled late on a side stream, consumers ordered
     # only by the waits the protocol makes, send pieces checked unchanged until completion): key ownership
