@@ -223,14 +223,19 @@ def state_from_packed(lo: int, hi: int) -> PState:
     return PState(tuple(cards), tuple(bonus), gems, (hi >> 41) & 0xFF, hi >> 49)
 
 
-def from_oracle(o, goal_pts, heuristic_name, beam_width) -> PySolve:
+def from_oracle(o, goal_pts, heuristic_name, beam_width, sample=None) -> PySolve:
     """A PySolve continuing the C oracle `o` from its newest beam: same queue, same trail, same MT state
-    (bench.py times one saturated step of it without replaying the early turns in Python)."""
+    (bench.py times one saturated step of it without replaying the early turns in Python).  sample = k: only
+    the beam's first k parents, and a trail of the newest beam's keys instead of every visited key (a bounded
+    timing sample of a wide turn: the Python trail of a W=4M solve would not fit; a child found in an older turn
+    is then scored and sorted as new, so the sample's rate errs low)."""
     t = o.nturns() - 1
-    lo, hi, _, _ = o.turn_arrays(t)
+    lo, hi, _, key = o.turn_arrays(t)
+    if sample is not None:
+        lo, hi = lo[:sample], hi[:sample]
     beam = [state_from_packed(a, b) for a, b in zip(lo.tolist(), hi.tolist())]
     ps = PySolve(goal_pts, use_heuristic=True, heuristic_name=heuristic_name, beam_width=beam_width,
                  mt_state625=o.mt_state())
-    ps.trail = set(o.visited_keys().view(np.int64).tolist())
+    ps.trail = set((key if sample is not None else o.visited_keys()).view(np.int64).tolist())
     ps.turns = [(beam, [None] * len(beam))]
     return ps

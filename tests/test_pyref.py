@@ -65,3 +65,22 @@ def test_seeded_solve_goal10_w1k():
     for g in golden('solves_small.json'):
         if g['goal'] == 10 and g['beam_width'] == 1000 and g['seed'] == 0 and g['heuristic'] in ('simple', 'efficiency'):
             _run(g)
+
+
+def test_from_oracle_sample_is_the_turns_prefix():
+    """bench.py's CPU baseline: the pure-Python step on the first k parents of the oracle's newest beam (same
+    config and MT state), with a trail of that beam's keys."""
+    import numpy as np
+    import oracle_c
+    random.seed(0)
+    o = oracle_c.OracleSolve(255, use_heuristic=True, heuristic_name='balanced', beam_width=2000,
+                             mt_state625=random.getstate()[1])
+    for _ in range(5):
+        o.step()
+    lo, hi, _, key = o.turn_arrays(o.nturns() - 1)
+    ps = pyref.from_oracle(o, 255, 'balanced', 2000, sample=50)
+    assert [s.key for s in ps.turns[0][0]] == np.asarray(key[:50]).view(np.int64).tolist()
+    assert len(ps.trail) == len(set(np.asarray(key).view(np.int64).tolist()))
+    r = ps.step()
+    assert r['n_parents'] == 50 and r['n_raw'] > 0 and 0 < r['n_kept'] <= 2000
+    o.close()
