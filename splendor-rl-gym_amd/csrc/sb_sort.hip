@@ -224,7 +224,10 @@ __device__ __forceinline__ void tk_pick_body(uint64_t* st) {
                            // count (prepass 89 -> 77 us, profiles/r3/s5/ab_topk.txt)
 #endif
 constexpr int TKH_NT = SB_TKH_NT;
-constexpr int TKH_NH = TKH_NT / 64 < 4 ? TKH_NT / 64 : 4;   // LDS sub-histograms (waves share them beyond 4)
+#ifndef SB_TKH_NH
+#define SB_TKH_NH 4   // LDS sub-histograms per select-histogram block (waves share them beyond this many)
+#endif
+constexpr int TKH_NH = TKH_NT / 64 < SB_TKH_NH ? TKH_NT / 64 : SB_TKH_NH;
 __global__ __launch_bounds__(TKH_NT) void k_tk_hist(const uint64_t* __restrict__ keys, int64_t n_host,
                                                    const uint64_t* __restrict__ n_dev, uint64_t* st, int only_fallback,
                                                    uint32_t* __restrict__ part, int pick) {
