@@ -432,7 +432,7 @@ class DistSolve:
             self._front_deferred = False
         if self.mig:
             return self._dedup_mig(st, off)
-        if c.world == 1 and hasattr(b, 'expand_defer'):
+        if c.world == 1 and hasattr(b, 'expand_defer') and not getattr(b, 'parts', 0):
             # one rank: no records, nothing to size, so no wait for the expansion; its raw count comes with
             # the apply's wait below
             b.expand_defer()
@@ -1021,6 +1021,9 @@ class HipBackend:
     # key ownership, world > 1: global-order claims (flags bit 11, sb_dist.inc k_claim_goc): own children become
     # records to this rank and all records are claimed in one pass in global order once every part has arrived
     GOC = os.environ.get('SB_DIST_GOC', '1') != '0'
+    # measurement aid: the world > 1 key-owner path (pipelined key pass, global-order claims) at world 1, so one
+    # GPU runs a rank's whole sharded device work with its streams overlapping as on an 8-GPU node (no exchange)
+    KP1 = os.environ.get('SB_DIST_KP1') == '1'
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
                  heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0,
@@ -1039,11 +1042,12 @@ class HipBackend:
             import warnings
             warnings.warn(self.MIG_CAVEAT, stacklevel=2)
         self.timing = bool(int(extra_flags) & 1)   # key-pass device time per step (sbd_keypass_ms)
-        self.goc = bool(self.GOC) and self.KEYPASS and world > 1 and not self.mig
+        xw = world > 1 or (self.KP1 and not self.mig)   # the world > 1 key-owner machinery (KP1: at world 1 too)
+        self.goc = bool(self.GOC or (world == 1 and self.KP1)) and self.KEYPASS and xw and not self.mig
         self.heur = bool(use_heuristic)
         cfg = L.SbConfig(goal_pts=int(goal_pts), use_heuristic=int(bool(use_heuristic)), heuristic=int(heuristic),
                          device=int(device_index), beam_width=int(beam_width), visited_log2=int(visited_log2),
-                         flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and world > 1 else 0) |
+                         flags=2 | (int(extra_flags) & 1201) | (64 if self.KEYPASS and xw else 0) |
                          (256 if self.mig else 0) | (512 if self.oe else 0) | (2048 if self.goc else 0),
                          world_size=int(world), rank=int(rank))
         h = C.c_void_p()
@@ -1056,7 +1060,7 @@ class HipBackend:
         torch.cuda.set_stream(self.stream)
         L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
         # world > 1: the pipelined key pass; received records are claimed on a second stream beside it
-        self.parts = max(1, min(16, self.PARTS)) if ((self.KEYPASS or self.mig) and world > 1) else 0
+        self.parts = max(1, min(16, self.PARTS)) if ((self.KEYPASS or self.mig) and xw) else 0
         self.cstream = None
         if self.parts:
             self.cstream = torch.cuda.Stream(self.device)
@@ -1187,7 +1191,7 @@ class HipBackend:
         world > 1: the pipelined key pass in self.parts exchange parts (n_global: the turn's parents over
         all ranks, bounds what this rank receives)."""
         self.world_x = int(world)
-        if self.parts and world > 1:
+        if self.parts and (world > 1 or self.KP1):
             self._chk(self.lib.sbd_expand_parts(self.h, int(world), int(self.parts), int(n_global)), 'sbd_expand_parts')
             return
         self._chk(self.lib.sbd_expand_launch(self.h, int(world)), 'sbd_expand_launch')

@@ -35,6 +35,8 @@ def _worker(rank, world, port, cfg, outdir):
         os.environ['SB_NOISE_CK'] = str(cfg['ck'])
     if 'keypass' in cfg:   # 0: the expansion kernel + separate owner partition (sbd_expand_launch) at world > 1
         os.environ['SB_DIST_KEYPASS'] = str(cfg['keypass'])
+    if cfg.get('kp1'):     # the world > 1 key-owner path at world 1 (HipBackend.KP1, a measurement aid)
+        os.environ['SB_DIST_KP1'] = '1'
     if 'gkr' in cfg:       # grouped kept records on the rebalance's wire (default on)
         os.environ['SB_DIST_GKR'] = '1' if cfg['gkr'] else '0'
     if 'parts' in cfg:     # exchange parts of the pipelined key pass (default 4)
@@ -129,6 +131,10 @@ CASES = [
     # answer buffer from the exact counts, mid-turn, with earlier parts' claims kept (sbd_grow_receive)
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'flags': 1024, 'parts': 4}),
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'flags': 1024 | 256}),
+    # the key-owner path (pipelined key pass, global-order claims of the own children as records) at world 1: the
+    # one-GPU measurement of a rank's sharded device work (bench.py SB_FORCE_DIST=1 SB_DIST_KP1=1)
+    (1, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'kp1': True}),
+    (1, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 9, 'heur': True, 'kp1': True, 'parts': 3}),
     # kept records on the rebalance's wire: the 20-byte records instead of (parent, destination) groups
     (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'gkr': False}),
     # Comm's RCCL branches against the engine's two streams, under RCCL's device-side completion contract
