@@ -33,11 +33,14 @@ def main():
                          'evenly); by default rank 0, which sends the most, as measured')
     ap.add_argument('--W', type=float, default=4e6, help='parents per rank')
     ap.add_argument('--parts', type=int, default=4, help='exchange parts of the key pass (SB_DIST_PARTS)')
+    ap.add_argument('--device-ms', type=float, default=None,
+                    help='device time per rank and step from another measurement (e.g. the world-1 key-pass run, '
+                         'profiles/busy_union.py) instead of the table\'s serialised total')
     a = ap.parse_args()
     t = json.load(open(a.table))
     b = [json.loads(l) for l in open(a.bench) if l.startswith('{')][-1]
     mean = t.get('robust_mean_ms', t['mean_ms'])   # launches that waited on another rank's work capped
-    dev = mean['device total (engine stream)']
+    dev = mean['device total (engine stream)'] if a.device_ms is None else a.device_ms
     keypass = mean.get('expand', 0.0)
     x = dict(b.get('exchange_MB_per_step_rank0', {}))
     if a.balanced_kept and 'kept records' in x:
