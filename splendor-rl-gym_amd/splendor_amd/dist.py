@@ -628,22 +628,30 @@ class DistSolve:
                         g_rec[:ans_base].copy_(rbuf[:ans_base])
                 ret, rbuf = g_ret, g_rec
             ostart = np.concatenate([[0], np.cumsum(cnt)])
+            # part j lands as [the other sources' pieces, in source order][this rank's own]: the own piece is a
+            # device copy on the claim stream, not a trip through the all_to_all (RCCL copies it slowly)
+            remote = from_src.copy()
+            remote[me] = 0
+            rtot = int(remote.sum())
             with ctx():
                 key = b.part_pack(j, int(ostart[-1]), send_base)
-                pieces = [key[int(ostart[o]):int(ostart[o + 1])] for o in range(W)]
-                _, hd = c.alltoall_pieces(pieces, from_src, what='records', out=rbuf[ans_base:need])
+                pieces = [key[int(ostart[o]):int(ostart[o + 1])] if o != me else key[:0] for o in range(W)]
+                _, hd = c.alltoall_pieces(pieces, remote, what='records', out=rbuf[ans_base:ans_base + rtot])
                 handles.append(hd)
+                if cnt[me]:
+                    rbuf[ans_base + rtot:need].copy_(key[int(ostart[me]):int(ostart[me + 1])])
             sends.append((cnt, send_base, ostart))
             recvs.append((from_src, ans_base))
             send_base += int(ostart[-1])
             ans_base = need
-        # virtual order: source q's records, part by part; segment (q, j) at physical ans_base_j + sum(from_src_j[:q])
+        # virtual order: source q's records, part by part; segment (q, j) at physical ans_base_j + the pieces of the
+        # other sources before q (this rank's own piece after all of them)
         vst, pst, vseg = [], [], {}
         v = 0
         for q in range(W):
             for j, (fs, ab) in enumerate(recvs):
                 vst.append(v)
-                pst.append(ab + int(fs[:q].sum()))
+                pst.append(ab + (int(fs.sum()) - int(fs[me]) if q == me else int(fs[:q].sum()) - (int(fs[me]) if q > me else 0)))
                 vseg[(q, j)] = v
                 v += int(fs[q])
         b.owner_total(ans_base)
