@@ -26,7 +26,7 @@ PHASES = [
     ('noise (side stream)', r'^k_mt_'),
     ('emit', r'^k_emit_w|^k_oe_(rowcnt|groups|pack|fix)'),
     ('joint select', r'^k_ds_|^k_tk_|^k_oe_ties'),
-    ('rebalance partition', r'^k_dest|^k_part_|^k_gkr_groups|^k_gkr_layout|^k_chunk_counts'),
+    ('rebalance partition', r'^k_dest|^k_part_|^k_gkr_groups|^k_gkr_layout|^k_gkr_scatter|^k_chunk_counts'),
     ('receive sort + gather', r'^k_recv_|^k_iota|^k_os_|^k_fx_|^k_copy_idx|^k_oe_recv|^k_oe_compose|^k_oe_merge|'
                               r'^k_gkr_flags|^k_gkr_expand|^k_gkr_cnt'),
 ]

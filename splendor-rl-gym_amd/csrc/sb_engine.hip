@@ -58,6 +58,12 @@ std::string oom_message(const char* what, size_t bytes, hipError_t code) {
     return m;
 }
 
+// SB_DEBUG_HBM_LIMIT (tests): allocations above it fail as if the HBM were full
+static bool debug_hbm_allows(size_t bytes) {
+    static const char* lim = std::getenv("SB_DEBUG_HBM_LIMIT");
+    return !lim || (double)bytes <= std::strtod(lim, nullptr);
+}
+
 void dev_malloc(void** p, size_t bytes, const char* what) {
     static const char* lim = std::getenv("SB_DEBUG_HBM_LIMIT");
     hipError_t e;
@@ -994,10 +1000,15 @@ static void grow_table(Engine& E, Entry*& tab, uint64_t& mask, double projected)
     SB_HIP(hipMemGetInfo(&freeb, &totalb));
     while (ncap > cap && ncap * sizeof(Entry) + GROW_RESERVE > freeb) ncap >>= 1;
     if (ncap == cap) return;
+    // Another process on the GPU (ranks sharing it) may take HBM between the sizing and the allocation: then a
+    // smaller table, or none — growth is ahead of need, and the HARD_LOAD check after the turn is the limit
     Entry* nt = nullptr;
-    const std::string what = "visited-set rebuild to " + std::to_string(ncap) + " slots (from " + std::to_string(cap) +
-                             "; free HBM at sizing " + gib((double)freeb) + ")";
-    dev_malloc((void**)&nt, ncap * sizeof(Entry), what.c_str());
+    for (; ncap > cap; ncap >>= 1) {
+        if (debug_hbm_allows(ncap * sizeof(Entry)) && hipMalloc((void**)&nt, ncap * sizeof(Entry)) == hipSuccess) break;
+        (void)hipGetLastError();
+        nt = nullptr;
+    }
+    if (!nt) return;
     SB_HIP(hipMemsetAsync(nt, 0xFF, ncap * sizeof(Entry), E.s));
     hipLaunchKernelGGL(k_rehash, dim3(grid_cap((int64_t)std::min<uint64_t>(cap, 1ull << 40), 256, 1u << 16)), dim3(256), 0,
                        E.s, tab, cap, nt, ncap - 1, E.d_small + 1);
