@@ -92,3 +92,21 @@ def test_sharded_slice_capacity_is_checked():
     rc = L.sb_create(ctypes.byref(cfg), np.zeros(625, np.uint32), 0, 0, ctypes.byref(h))
     assert rc == _lib.SB_ERR_CAPACITY
     assert b'2^26' in L.sb_last_error()
+
+
+def test_sharded_entry_points_refuse_a_null_engine():
+    """Every sharded entry point (sbd_*) the header declares answers a null engine with SB_ERR_ARG before
+    touching the device: arguments typed from the header's own parameter lists, all zero / null."""
+    _lib.lib()
+    L = ctypes.CDLL(_lib.LIB_PATH)   # fresh function objects: no argtypes another test's backend may have set
+    text = open(HEADER).read()
+    probed = 0
+    for m in re.finditer(r'^\s*int\s+(sbd_\w+)\s*\(([^)]*)\)\s*;', text, re.M):
+        name, params = m.group(1), [p.strip() for p in m.group(2).split(',')]
+        args = [ctypes.c_void_p(None) if '*' in p else ctypes.c_int64(0) if 'int64' in p else ctypes.c_int32(0)
+                for p in params]
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        assert f(*args) == _lib.SB_ERR_ARG, name
+        probed += 1
+    assert probed == len([s for s in declared_symbols() if s.startswith('sbd_')])
