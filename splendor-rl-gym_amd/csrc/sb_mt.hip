@@ -246,6 +246,9 @@ constexpr int JMP_JG = 10;                 // 624 outputs in groups of 64
 // bits needs y over [i0 + 1, i0 + JR_S + 624]; wave w accumulates the outputs of groups w, w+4, w+8 in
 // registers.  Runs beside the step's kernels on the side stream: 87 KB of LDS per CU had held the
 // expansion and the select to fewer resident blocks while it ran.
+#ifndef SB_JR_WIDE
+#define SB_JR_WIDE 1   // 0: one LDS read per set poly bit (the round-2 loop)
+#endif
 #ifndef SB_JR_NT
 #define SB_JR_NT 1024   // A/B profiles/r2_ab_mt_nt.txt: 256 / 640 / 1024 threads
 #endif
@@ -254,13 +257,15 @@ constexpr int JR_NW = JR_NT / 64, JR_Q = (JMP_JG + JR_NW - 1) / JR_NW;   // outp
 static_assert(JR_RING >= 2 * JR_S + 624 + 227 + 1, "ring holds the block being read and the next one");
 __global__ __launch_bounds__(JR_NT) void k_mt_jump(const uint32_t* win_in, uint32_t* win_out, int src0, int dst0,
                                                     const uint32_t* __restrict__ gpoly) {
-    __shared__ uint32_t ring[JR_RING];
+    __shared__ uint32_t ring[JR_RING + 32];   // + a mirror of slots 0..31: a word's 32 reads never wrap
     __shared__ uint32_t gp[624];
     constexpr int M = JR_RING - 1;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int64_t src = src0 + blockIdx.x, dst = dst0 + blockIdx.x;
     for (int i = t; i < 624; i += JR_NT) {
-        ring[i] = win_in[src * 624 + i];
+        const uint32_t v = win_in[src * 624 + i];
+        ring[i] = v;
+        if (SB_JR_WIDE && i < 32) ring[JR_RING + i] = v;
         gp[i] = gpoly[i];
     }
     __syncthreads();
@@ -272,7 +277,12 @@ __global__ __launch_bounds__(JR_NT) void k_mt_jump(const uint32_t* win_in, uint3
         const int need = i0 + JR_S + 625;   // y indices read by this block: [i0 + 1, i0 + JR_S + 624]
         while (have < need) {   // y_{k+624} = f(y_k, y_{k+1}, y_{k+397}), 227 at a time
             const int k = have - 624 + t;
-            if (t < 227) ring[(k + 624) & M] = mt_mix(ring[k & M], ring[(k + 1) & M], ring[(k + 397) & M]);
+            if (t < 227) {
+                const int d = (k + 624) & M;
+                const uint32_t v = mt_mix(ring[k & M], ring[(k + 1) & M], ring[(k + 397) & M]);
+                ring[d] = v;
+                if (SB_JR_WIDE && d < 32) ring[JR_RING + d] = v;
+            }
             have += 227;
             __syncthreads();
         }
@@ -285,12 +295,26 @@ __global__ __launch_bounds__(JR_NT) void k_mt_jump(const uint32_t* win_in, uint3
             const int jj = j < 624 ? j : 623;
             uint32_t a = acc[q];
             for (int wi = i0 / 32; wi < wend; wi++) {
+#if SB_JR_WIDE
+                // all 32 words of the slice read at once (immediate offsets from one masked base, no wrap
+                // thanks to the mirror), the poly bits applied as wave-uniform masks: the loads pipeline
+                // instead of one LDS round trip per set bit
+                const uint32_t bits = __builtin_amdgcn_readfirstlane(gp[wi]);
+                if (!bits) continue;
+                const uint32_t* r = ring + ((1 + wi * 32 + jj) & M);
+                uint32_t v[32];
+#pragma unroll
+                for (int b = 0; b < 32; b++) v[b] = r[b];
+#pragma unroll
+                for (int b = 0; b < 32; b++) a ^= v[b] & (0u - ((bits >> b) & 1u));
+#else
                 uint32_t bits = gp[wi];   // wave-uniform
                 while (bits) {
                     const int b = __builtin_ctz(bits);
                     bits &= bits - 1;
                     a ^= ring[(1 + wi * 32 + b + jj) & M];
                 }
+#endif
             }
             acc[q] = a;
         }
