@@ -231,7 +231,9 @@ int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts,
  * the answers must come back in for sbd_apply).  Received records claim with answer indices in arrival
  * order (sbd_owner_claim, on the claim stream, beside the later parts' kernels); sbd_owner_total sets the
  * turn's received count before sbd_owner_finish. */
-int sbd_expand_parts(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global);
+/* bounds (nullable): nparts + 1 local parent indices, part j = parents [bounds[j], bounds[j+1]) — block-cyclic slices,
+ * where part j of rank r is block j * world + r of the global queue; null: parts of equal 64-parent chunk counts */
+int sbd_expand_parts(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const int64_t* bounds);
 int sbd_part_counts(sb_engine* e, int32_t part, int64_t* owner_counts, int64_t* recv_capacity);
 int sbd_part_pack(sb_engine* e, int32_t part, uint64_t* d_key, int64_t send_base);
 int sbd_set_claim_stream(sb_engine* e, void* stream);
@@ -264,6 +266,14 @@ int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
  * include them). */
 int sbd_owner_claim_all(sb_engine* e, const uint64_t* d_key, int64_t n_total, int32_t nseg, const int64_t* v_start,
                         const int64_t* p_start, uint8_t* d_ret);
+/* global-order claims of one exchange part as soon as it has arrived (block-cyclic slices, or world 1: part j of every
+ * source is one contiguous range of the global order, after every earlier part): virtual records [v_begin, v_end) in
+ * nseg <= 64 segments (v_start[0] = v_begin ascending, record v at d_key + p_start[k] + v - v_start[k]), tag turn | v,
+ * d_ret[v]; on the claim stream, after the caller's wait for the part's transfer; part < 16 selects its ticket word.
+ * d_ret is final for a part once every later part's claims have run (a later record may displace; sbd_pack_bits_segs
+ * drops the displaced answers). */
+int sbd_owner_claim_part(sb_engine* e, int32_t part, const uint64_t* d_key, int64_t v_begin, int64_t v_end, int32_t nseg,
+                         const int64_t* v_start, const int64_t* p_start, uint8_t* d_ret);
 /* answers over the wire as bits: dst[i] = bit k set iff src[8i + k] != 0 (n bytes -> ceil(n/8));
  * unpack is the inverse (n answer bytes from ceil(n/8) packed bytes).  Both on the engine stream. */
 int sbd_pack_bits(sb_engine* e, const uint8_t* d_src, int64_t n, uint8_t* d_dst);
@@ -300,15 +310,21 @@ int sbd_noise_chunk(sb_engine* e, int32_t slot, void* counts_out);          /* d
 int sbd_noise_sync(sb_engine* e);                                          /* wait for sbd_noise_chunk */
 int sbd_noise_pack(sb_engine* e, int32_t m, const int64_t* idx, void* wins_out);
 int sbd_noise_fill(sb_engine* e, int32_t m, const void* wins, const uint64_t* acc0, uint64_t a, uint64_t b);
+/* block-cyclic slices: the accepted draws of nr <= 16 ranges [a[k], b[k]) (this rank's blocks of the next_queue), range k
+ * kept at ring position dst[k] + (index - a[k]) (the emission reads local position k at consumed + k_off + k) */
+int sbd_noise_fill_ranges(sb_engine* e, int32_t m, const void* wins, const uint64_t* acc0, int32_t nr, const uint64_t* a,
+                          const uint64_t* b, const uint64_t* dst);
 
 /* Joint select on the device (dist.py _multiselect), no host round trip: sbd_key_range writes this
  * rank's score-key range of the turn to range_dev as two int64 for one all_reduce(MIN) by the caller
- * (kmin ^ 2^63, ~(kmax ^ 2^63)); sbd_sel_begin = select state for npos (<= 15) positions (1-based ranks
+ * (kmin ^ 2^63, ~(kmax ^ 2^63)); sbd_sel_begin = select state for npos (<= 64) positions (1-based ranks
  * in score-descending order) below the bits common to the reduced range; per pass: sbd_sel_hist
- * (npos x 1024 int64 histogram of the next 10-bit digit per distinct prefix into hist_dev, over the keys
+ * (npos x 1024 int64 buffer: a histogram of the next digit — 10 bits while at most 16 prefixes are live, else 8 —
+ * per distinct prefix into hist_dev, over the keys
  * (src 0) or the candidates (src 1); hist_dev must be zero on entry: fresh, or as the previous
  * sbd_sel_pick left it), an all_reduce(SUM) of hist_dev by the caller on the same stream,
- * sbd_sel_pick; passes after the last digit are no-ops, so the caller runs a fixed 7 (ceil(64/10)).
+ * sbd_sel_pick; passes after the last digit are no-ops, so the caller runs a fixed 7 (ceil(64/10)), 8 when
+ * npos > 16 (8-bit digits).
  * After the first pass sbd_sel_compact keeps the keys of the chosen buckets as candidates.
  * sbd_sel_eq: count of keys equal to position 0's key (int64 at eq_dev) for the all_gather of the
  * keep boundary's ties. */
@@ -324,6 +340,20 @@ int sbd_sel_eq(sb_engine* e, void* eq_dev);
 int sbd_partition(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t nsplit, int32_t world,
                   void* dest_counts_dev);
 int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t world, void* dest_counts_dev);
+/* ---- block-cyclic slices (key ownership, per-part claims): rank r's slice is nblk blocks, block j = global block
+ * j * world + r (the next beam dealt so, every rank holds parents of every score level and each exchange part is one
+ * range of the global order).  sbd_block_counts (after sbd_apply): survivors per local block (bounds = nblk + 1 local
+ * parents) to out_dev (nblk int64).  sbd_sel_eq_blocks: the keep boundary's ties per local block (qstart = nblk + 1
+ * local next_queue starts) to eq_dev (nblk int64), and the per-tile offsets the partition reads.
+ * sbd_partition_blocks: kept test with this rank's quota from every rank's per-block ties (eq_all_dev: world x nblk,
+ * rank-major; ties kept in global (block, rank) order), the select's positions 1 .. world * nblk - 1 as the next
+ * beam's block boundaries; digit = destination rank * nblk + its block; dest_counts_dev = world * nblk int64.
+ * sbd_dest_subcounts: the kept records per (local block, digit), nblk x D int64 (the receiver's ordering). */
+int sbd_block_counts(sb_engine* e, int32_t nblk, const int64_t* bounds, void* out_dev);
+int sbd_sel_eq_blocks(sb_engine* e, int32_t nblk, const int64_t* qstart, void* eq_dev);
+int sbd_partition_blocks(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t world, int32_t nblk,
+                         void* dest_counts_dev);
+int sbd_dest_subcounts(sb_engine* e, int32_t nblk, const int64_t* qstart, int32_t D, void* out_dev);
 /* kept records grouped by destination, next_queue order inside a group, one all_to_all buffer of at least the
  * kept count (the local next_queue size always suffices, so it can be enqueued before the counts reach the host).
  * 3 x u64 per record (state lo, state hi, global parent rank | noise draw << 32: the receiver re-scores it);
@@ -343,7 +373,12 @@ int sbd_pack_kept_grouped(sb_engine* e, uint32_t* d_buf, int64_t cap_u32, int64_
  * each, in source order) expanded into the 20-byte records sbd_receive takes (d_rec: sum(children) x 5 u32, the
  * sources' segments concatenated in order).  Error word bit 256 if a segment's group starts do not match its rows. */
 int sbd_unpack_kept(sb_engine* e, const uint32_t* d_buf, int32_t nseg, const int64_t* seg_base, const int64_t* seg_groups,
-                    const int64_t* seg_children, uint32_t* d_rec);
+                    const int64_t* seg_children, uint32_t* d_rec, int32_t nperm, const int64_t* perm, int32_t npm,
+                    const int64_t* pmap);
+/* (block-cyclic slices: perm = nperm (source child, destination record) run starts — the children of each (source,
+ * destination part, source block) run written in (destination part, source block, source) order, the global
+ * next_queue order within a block; pmap = npm (sender-side parent number, global rank) run starts, the senders'
+ * rank-major numbering mapped to the global queue.  Both nullable with n = 0.) */
 /* the new slice: n received records in the form sbd_pack_kept wrote (global next_queue order, or with owner
  * emission source segments in position order), stable-sorted by score if heur */
 int sbd_receive(sb_engine* e, const uint64_t* d_rec, int64_t n, int32_t heur);

@@ -918,6 +918,7 @@ struct Engine {
     DBuf<uint8_t> snv;                    // sharded emission: each survivor's noise draw (3-word kept records)
     DBuf<uint8_t> gdig;                   // grouped kept records: group starts by destination
     DBuf<uint32_t> gk_hist, gk_off, gk_cnt, gk_coff;   // ... group partition, buffer layout; receive: start flags, scan
+    DBuf<uint64_t> gk_tab;                // ... receive (block-cyclic slices): the permutation and parent-map runs
     DBuf<uint64_t> rkey2;                 // owner emission: received records' re-scored keys, arrival order
     bool sdesc = false, sdesc32 = false;  // sharded emission wrote descriptors (4-byte when sdesc32) into nlo
     int64_t sdesc_goff = 0;               // ... global ranks: the slice's parents start at this one
@@ -947,6 +948,9 @@ struct Engine {
     uint64_t* h_goc = nullptr;            // pinned staging of it
     int ks_parts = 0;
     int64_t ks_c[17] = {};
+    int64_t ks_pb[17] = {};               // each part's first local parent (ks_pb[ks_parts] = n): chunk c of part j holds
+                                          // parents ks_pb[j] + 64 (c - ks_c[j]) .. (block-cyclic parts: any bounds)
+    bool ks_bounds = false;               // this turn's parts came from the caller's bounds (block-cyclic slices)
     size_t ks_ccoff[17] = {};
     uint64_t ks_sbase[17] = {};           // each part's first index in the turn's send buffers (sbd_part_pack)
     struct KpTab* h_kt = nullptr;         // pinned: the apply's answer-place table (global-order claims)

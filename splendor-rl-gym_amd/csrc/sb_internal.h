@@ -220,7 +220,11 @@ void noise_shard_chunk(NoiseStream& ns, int slot, uint32_t* d_counts, hipStream_
 // gather checkpoint windows (index = slot * P * S + sub-segment) into d_out (m x 624)
 void noise_shard_pack(NoiseStream& ns, int m, const int64_t* h_idx, uint32_t* d_out, hipStream_t st);
 // regenerate m sub-segments from contiguous windows; accepted values with global index in [a, b) go to the ring
-void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+struct NoiseRanges {   // sharded fill: accepted-draw index ranges [a, b) placed at ring positions dst + (idx - a)
+    uint64_t a[16], b[16], dst[16];
+    int n;
+};
+void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, const NoiseRanges& R,
                       hipStream_t st);
 void noise_mt_state(NoiseStream& ns, uint32_t* out625);
 // debug: raw device words from P producers of `twists` twists per segment

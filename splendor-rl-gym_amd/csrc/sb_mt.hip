@@ -191,9 +191,13 @@ __global__ __launch_bounds__(256) void k_mt_place(const uint8_t* __restrict__ st
 // Sharded streams: block j regenerates one sub-segment (twists twists) from window j of wins (624
 // words each); its first accepted draw has global index seg_acc0[j].  Accepted values with global
 // index in [a, b) go to ring[index & ring_mask]; the block stops once past b.
+// ranges of accepted-draw indices [a[k], b[k]) this rank emits with, each placed at ring position dst[k] + (idx - a[k])
+// (one range at its own index for contiguous slices; block-cyclic slices: a range per block, placed in local order)
 __global__ __launch_bounds__(640) void k_mt_fill(const uint32_t* __restrict__ wins, const uint64_t* __restrict__ seg_acc0,
-                                                  int64_t twists, uint64_t a, uint64_t b, uint8_t* __restrict__ ring,
+                                                  int64_t twists, const NoiseRanges R, uint8_t* __restrict__ ring,
                                                   uint64_t ring_mask) {
+    uint64_t b = 0;
+    for (int k = 0; k < R.n; k++) b = R.b[k] > b ? R.b[k] : b;
     __shared__ uint32_t buf[2][624];
     __shared__ uint32_t wc[10];
     const int t = threadIdx.x, wv = t >> 6;
@@ -225,7 +229,9 @@ __global__ __launch_bounds__(640) void k_mt_fill(const uint32_t* __restrict__ wi
             total += c;
         }
         const uint64_t idx = run + before + __popcll(m & lanemask_lt());
-        if (acc && idx >= a && idx < b) ring[idx & ring_mask] = (uint8_t)((y >> 25) + 1);
+        if (acc)
+            for (int k = 0; k < R.n; k++)
+                if (idx >= R.a[k] && idx < R.b[k]) ring[(R.dst[k] + (idx - R.a[k])) & ring_mask] = (uint8_t)((y >> 25) + 1);
         run += total;
         cur ^= 1;
         __syncthreads();   // wc is rewritten by the next twist
@@ -561,12 +567,12 @@ void noise_shard_pack(NoiseStream& ns, int m, const int64_t* h_idx, uint32_t* d_
     SB_HIP(hipGetLastError());   // (pageable-source copy above completes before returning)
 }
 
-void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, uint64_t a, uint64_t b,
+void noise_shard_fill(NoiseStream& ns, int m, const uint32_t* d_wins, const uint64_t* h_acc0, const NoiseRanges& R,
                       hipStream_t st) {
-    if (m <= 0 || a >= b) return;
+    if (m <= 0 || R.n <= 0) return;
     ns.segtab.ensure((size_t)m);
     SB_HIP(hipMemcpyAsync(ns.segtab.p, h_acc0, (size_t)m * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_mt_fill, dim3(m), dim3(640), 0, st, d_wins, ns.segtab.p, (int64_t)ns.ck, a, b, ns.ring.p,
+    hipLaunchKernelGGL(k_mt_fill, dim3(m), dim3(640), 0, st, d_wins, ns.segtab.p, (int64_t)ns.ck, R, ns.ring.p,
                        ns.ring_mask);
     SB_HIP(hipGetLastError());
 }

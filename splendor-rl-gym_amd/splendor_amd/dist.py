@@ -46,6 +46,12 @@ BIG = (1 << 62)
 
 # grouped kept records on the rebalance's wire (key ownership, world > 1): SB_DIST_GKR=0 sends the 20-byte records
 GKR = os.environ.get('SB_DIST_GKR', '1') != '0'
+# block-cyclic slices (key ownership with global-order claims, beam search): the next beam is dealt to the ranks in
+# world x parts blocks, block b to rank b % world as its part b // world.  Part j of every rank is then one contiguous
+# range of the global order, after every earlier part, so its claims run as soon as it has arrived (beside the next
+# parts' key pass), and every rank holds parents of every score level (the kept records leave every rank about evenly).
+# SB_DIST_BC=0: contiguous rank ranges (claims after the last part)
+BC = os.environ.get('SB_DIST_BC', '1') != '0'
 
 class Comm:
     """torch.distributed helpers; gloo works on CPU tensors (device tensors are staged)."""
@@ -277,8 +283,11 @@ class ShardNoise:
         js = np.arange(j0, j1, dtype=np.int64)
         return js[(cum[js + 1] > cum[js]) & (cum[js + 1] > a - s0)]
 
-    def prepare(self, A: int, N: int, all_n: np.ndarray):
-        """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission."""
+    def prepare(self, A: int, N: int, all_n: np.ndarray, blocks: np.ndarray | None = None):
+        """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission (k_off = the
+        next_queue entries of the ranks before it).  blocks (block-cyclic slices, (world, parts) entries per block):
+        this rank's draws are those of its blocks' global next_queue ranges, placed at local positions k_off + its
+        earlier blocks' entries."""
         c, b = self.c, self.b
         # the round in flight is gathered only once its draws are needed (the same decision on every
         # rank: gen_total and A + N are global), so its generation overlaps whole steps instead of the
@@ -289,14 +298,22 @@ class ShardNoise:
             self._launch()
             self._collect()
         starts = A + np.concatenate([[0], np.cumsum(all_n)]).astype(np.int64)
-        me, PS = c.rank, self.P * self.S
-        send = [[] for _ in range(c.world)]
-        recv = [[] for _ in range(c.world)]
+        me, PS, G = c.rank, self.P * self.S, c.world
+        if blocks is None:   # rank r: [starts[r], starts[r + 1]), kept at its own index
+            ranges = [[(int(starts[r]), int(starts[r + 1]), int(starts[r]))] for r in range(G)]
+        else:                # rank r: its blocks (j, r), global order (j, r) j-major; local order j
+            nb = blocks.shape[1]
+            gq = A + np.concatenate([[0], np.cumsum(blocks.T.reshape(-1))]).astype(np.int64)
+            lq = np.concatenate([np.zeros((G, 1), np.int64), np.cumsum(blocks, axis=1)], axis=1)
+            ranges = [[(int(gq[j * G + r]), int(gq[j * G + r + 1]), int(starts[r] + lq[r, j])) for j in range(nb)]
+                      for r in range(G)]
+        send = [[] for _ in range(G)]
+        recv = [[] for _ in range(G)]
         for s0, cum, g, slot in self.chunks:
-            for r in range(c.world):
+            for r in range(G):
                 if g != me and r != me:
                     continue
-                js = self._subsegs(s0, cum, int(starts[r]), int(starts[r + 1]))
+                js = np.unique(np.concatenate([self._subsegs(s0, cum, a, e) for a, e, _ in ranges[r]]))
                 if g == me:
                     send[r].append(slot * PS + js)
                 if r == me:
@@ -307,7 +324,10 @@ class ShardNoise:
         wins = b.noise_pack(cat(send))
         if c.world > 1:
             wins = c.alltoall(wins, [len(x) for x in send], [len(x) for x in recv], what='noise windows')
-        b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
+        if blocks is None:
+            b.noise_fill(wins, cat(recv), int(starts[me]), int(starts[me + 1]))
+        else:
+            b.noise_fill_ranges(wins, cat(recv), [x for x in ranges[me] if x[1] > x[0]])
         self.chunks = [ch for ch in self.chunks if ch[0] + ch[1][-1] > A + N]
         self._ahead = A + N + 4 * N   # background() launches the next round below this mark
 
@@ -339,6 +359,14 @@ class DistSolve:
         # owner emission (with card-set ownership): survivors emitted on the expanding ranks, whose parents span
         # every score level, so the kept records leave every rank evenly (HipBackend.OE / sb_oe.inc)
         self.oe = self.mig and bool(getattr(backend, 'oe', False))
+        # block-cyclic slices (BC): parts = blocks of the global queue, claims per part, the next beam dealt in blocks
+        P = int(getattr(backend, 'parts', 0) or 0)
+        self.bc = (BC and use_heuristic and bool(getattr(backend, 'goc', False)) and not self.mig and P >= 2 and
+                   comm.world * P <= 64 and hasattr(backend, 'partition_blocks') and (comm.world == 1 or GKR))
+        self.nb = P if self.bc else 1           # blocks per rank
+        self.blocks = []                        # per turn: (world, nb) block sizes, block (r, j) = global block j * world + r
+        n0 = int(backend.n_local())
+        self._bounds = [0] + [n0] * self.nb     # this rank's local block bounds of the slice being expanded
         self._launch_front(1)                   # runs while the host does the turn sync / goal check (the root)
         self.lookahead = True                   # step() launches the next turn's expansion before returning
         self._front_deferred = False            # lookahead was off: the next step() launches it
@@ -352,11 +380,43 @@ class DistSolve:
         """The next turn's front half, enqueued without a wait: the expansion (key-owner protocol); with card-set
         ownership the parents' owner digits and partition counts, which _turn_sync always launches itself."""
         if not self.mig:
-            self.b.expand_launch(self.c.world, n_global)
+            if self.bc:
+                self.b.expand_launch(self.c.world, n_global, bounds=self._bounds)
+            else:
+                self.b.expand_launch(self.c.world, n_global)
 
     def offset(self, turn=None) -> int:
+        """This rank's first parent in the rank-major numbering of turn's queue (the emission's parent numbers; with
+        block-cyclic slices the receiver maps them to global ranks)."""
         cnt = self.counts[self.turn if turn is None else turn]
         return int(cnt[:self.c.rank].sum())
+
+    def layout(self, turn):
+        """(gstart, lstart) of turn's queue: gstart[r, j] = global position of rank r's block j, lstart[r] = its local
+        block bounds (nb + 1).  Contiguous slices: one block per rank."""
+        bs = self.blocks[turn]
+        G, B = bs.shape
+        gq = np.concatenate([[0], np.cumsum(bs.T.reshape(-1))]).astype(np.int64)
+        gstart = gq[:-1].reshape(B, G).T
+        lstart = np.concatenate([np.zeros((G, 1), np.int64), np.cumsum(bs, axis=1)], axis=1)
+        return gstart, lstart
+
+    def locate(self, turn, g):
+        """(owner rank, local index) of global queue position g of turn."""
+        bs = self.blocks[turn]
+        G, B = bs.shape
+        ends = np.cumsum(bs.T.reshape(-1))
+        k = int(np.searchsorted(ends, g, side='right'))
+        r, j = k % G, k // G
+        gstart, lstart = self.layout(turn)
+        return r, int(lstart[r, j] + g - gstart[r, j])
+
+    def global_order(self, turn):
+        """[(rank, local start, length)] runs of turn's queue in global order (tests reassemble the slices with it)."""
+        bs = self.blocks[turn]
+        G, B = bs.shape
+        _, lstart = self.layout(turn)
+        return [(r, int(lstart[r, j]), int(bs[r, j])) for j in range(B) for r in range(G)]
 
     # ------------------------------------------------------------ goal check (src/solver.py:438-445)
     def _turn_sync(self):
@@ -368,6 +428,8 @@ class DistSolve:
         gt = self.b.goal_table().astype(np.int64)
         if self.mig:   # the slice's parents and raw children per card-set owner travel with the turn sync
             extra = self.b.mig_counts()
+        elif self.bc:  # the slice's block sizes
+            extra = np.diff(np.asarray(self._bounds, dtype=np.int64))
         M = self.c.allgather_array(np.concatenate([[self.b.n_local()], gt, extra]), host=True)
         if self.mig:
             W = self.c.world
@@ -375,10 +437,20 @@ class DistSolve:
             self._mig_R = M[:, 257 + W:257 + 2 * W].copy()    # [source][owner] their raw children
             M = M[:, :257]
         cnt = M[:, 0].copy()
-        offs = np.concatenate([[0], np.cumsum(cnt)[:-1]])
-        first = M[:, 1:]
+        self.blocks.append(M[:, 257:257 + self.nb].copy() if self.bc else cnt[:, None].copy())
+        assert (self.blocks[-1].sum(axis=1) == cnt).all(), 'block sizes disagree with the slice sizes'
+        first = M[:, 1:257]
         self.counts.append(cnt)
-        self._goal_g = np.where(first != NONE32, first + offs[:, None], BIG).min(axis=0)
+        # the first local position per pts -> global position (its block's global start + the offset in the block)
+        gstart, lstart = self.layout(len(self.blocks) - 1)
+        glob = np.full(first.shape, BIG, dtype=np.int64)
+        for r in range(first.shape[0]):
+            ok = first[r] != NONE32
+            if ok.any():
+                loc = first[r][ok]
+                j = np.searchsorted(lstart[r, 1:], loc, side='right')
+                glob[r][ok] = gstart[r, j] + loc - lstart[r, j]
+        self._goal_g = glob.min(axis=0)
 
     def _goal_check(self, st):
         g = self._goal_g
@@ -581,7 +653,13 @@ class DistSolve:
 
     def _dedup_parts(self, st, off):
         back = self._exchange_parts_goc(st) if getattr(self.b, 'goc', False) else self._exchange_parts(st)
-        all_n = self.c.gather_dev(self.b.apply(back)).astype(np.int64)   # the apply's count: one wait for both
+        n_dev = self.b.apply(back)
+        if self.bc:   # survivors per block (their sum is the apply's count): one wait for all
+            allb = self.c.gather_dev(self.b.block_counts(self._bounds)).astype(np.int64).reshape(self.c.world, self.nb)
+            self._allb = allb
+            all_n = allb.sum(axis=1)
+        else:
+            all_n = self.c.gather_dev(n_dev).astype(np.int64)   # the apply's count: one wait for both
         self.b.apply_finish(int(all_n[self.c.rank]))
         self._mark(st, 'dedup_exchange')
         return self._post_dedup(st, all_n, off)
@@ -602,6 +680,7 @@ class DistSolve:
         send_base = ans_base = 0
         ret = rbuf = None
         cap = 0
+        bc = self.bc
         for j in range(P):
             cnt, cap_j = b.part_counts(j)                     # waits for part j's key pass only; self included
             extra = [b.raw_total()] if j == 0 else []
@@ -626,6 +705,8 @@ class DistSolve:
                     g_ret, g_rec = b.answer_buffer(cap), b.record_buffer(cap)
                     if ans_base:
                         g_rec[:ans_base].copy_(rbuf[:ans_base])
+                        if bc:   # the earlier parts' answers (claimed already)
+                            g_ret[:ans_base].copy_(ret[:ans_base])
                 ret, rbuf = g_ret, g_rec
             ostart = np.concatenate([[0], np.cumsum(cnt)])
             # part j lands as [the other sources' pieces, in source order][this rank's own]: the own piece is a
@@ -640,6 +721,15 @@ class DistSolve:
                 handles.append(hd)
                 if cnt[me]:
                     rbuf[ans_base + rtot:need].copy_(key[int(ostart[me]):int(ostart[me + 1])])
+                if bc:   # block-cyclic: part j is the global order's next range — claim it now, sources in order
+                    vs, ps, v = [], [], ans_base
+                    for q in range(W):
+                        vs.append(v)
+                        ps.append(ans_base + (rtot if q == me else int(remote[:q].sum())))
+                        v += int(from_src[q])
+                    c.wait(hd)                                # RCCL: the claim stream waits for the part's transfer
+                    handles[-1] = None
+                    b.owner_claim_part(j, rbuf, ans_base, need, vs, ps, ret)
             sends.append((cnt, send_base, ostart))
             recvs.append((from_src, ans_base))
             send_base += int(ostart[-1])
@@ -647,18 +737,24 @@ class DistSolve:
         # virtual order: source q's records, part by part; segment (q, j) at physical ans_base_j + the pieces of the
         # other sources before q (this rank's own piece after all of them)
         vst, pst, vseg = [], [], {}
-        v = 0
-        for q in range(W):
+        if bc:   # virtual order (part, source, record): every part claimed on arrival above
             for j, (fs, ab) in enumerate(recvs):
-                vst.append(v)
-                pst.append(ab + (int(fs.sum()) - int(fs[me]) if q == me else int(fs[:q].sum()) - (int(fs[me]) if q > me else 0)))
-                vseg[(q, j)] = v
-                v += int(fs[q])
+                for q in range(W):
+                    vseg[(q, j)] = ab + int(fs[:q].sum())
+        else:
+            v = 0
+            for q in range(W):
+                for j, (fs, ab) in enumerate(recvs):
+                    vst.append(v)
+                    pst.append(ab + (int(fs.sum()) - int(fs[me]) if q == me else int(fs[:q].sum()) - (int(fs[me]) if q > me else 0)))
+                    vseg[(q, j)] = v
+                    v += int(fs[q])
         b.owner_total(ans_base)
         with ctx():
-            for hd in handles:
-                c.wait(hd)                                    # RCCL: the claim stream waits for every transfer
-            b.owner_claim_all(rbuf, ans_base, vst, pst, ret)
+            if not bc:
+                for hd in handles:
+                    c.wait(hd)                                # RCCL: the claim stream waits for every transfer
+                b.owner_claim_all(rbuf, ans_base, vst, pst, ret)
             b.owner_finish(ret)
         if cs is not None:
             torch.cuda.current_stream().wait_stream(cs)
@@ -793,7 +889,7 @@ class DistSolve:
         self._oe_noise_done = False
         if not oe:   # (owner emission: the range ranks' draws went out with the offsets, _oe_emit)
             if self.heur:
-                self.noise.prepare(self.consumed, N, all_n)
+                self.noise.prepare(self.consumed, N, all_n, self._allb if self.bc else None)
                 self.consumed += N
             self._mark(st, 'noise')
             b.emit(k_off, N, off)
@@ -802,7 +898,8 @@ class DistSolve:
         G = c.world
         if self.heur:
             has_top = N > self.W
-            pos = ([self.W] if has_top else []) + [max(1, -(-j * K // G)) for j in range(1, G)]
+            nsp = G * self.nb   # destination ranges: the ranks, or (block-cyclic) the next beam's world x parts blocks
+            pos = ([self.W] if has_top else []) + [max(1, -(-j * K // nsp)) for j in range(1, nsp)]
             eq_all = None
             if pos:
                 self._multiselect(pos, st)
@@ -811,11 +908,15 @@ class DistSolve:
                     tp, need = b.oe_ties()
                     allt = c.allgather_var(tp)
                     pstar = int(np.partition(allt, need - 1)[need - 1]) if need > 0 else -1
+                elif has_top and self.bc:   # ties per block: kept in global (block, rank) order
+                    eq_all = c.allgather_tensor(b.sel_eq_blocks(self._qstart())).reshape(-1)
                 elif has_top:
                     eq_all = c.allgather_tensor(b.sel_eq()).reshape(-1)
             self._mark(st, 'sel_eq')
             if oe:
                 dest_dev = b.oe_partition(has_top, pstar if has_top else -1, len(pos) - int(has_top), G)
+            elif self.bc:
+                dest_dev = b.partition_blocks(has_top, eq_all, c.rank, G, self.nb)
             else:
                 dest_dev = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
         elif oe:
@@ -826,7 +927,10 @@ class DistSolve:
         # 20-byte kept records when every global parent rank of the turn fits 25 bits (the same choice on every rank);
         # world > 1 with key ownership: grouped by (parent, destination) on the wire (sbd_pack_kept_grouped)
         rec20 = st['n_parents'] <= (1 << 25)
-        if GKR and c.world > 1 and rec20 and not oe and not self.mig and hasattr(b, 'pack_kept_grouped'):
+        if self.bc and c.world > 1:
+            assert rec20, 'block-cyclic slices need global parent ranks below 2^25 (20-byte records)'
+            self._rebalance_grouped_bc(st, all_n)
+        elif GKR and c.world > 1 and rec20 and not oe and not self.mig and hasattr(b, 'pack_kept_grouped'):
             self._rebalance_grouped(st, all_n)
         else:
             self._rebalance(st, all_n, K, dest_dev, oe, rec20)
@@ -867,10 +971,69 @@ class DistSolve:
         rrec = b.unpack_kept(rbuf, ro[:-1], recv2[:, 1], recv2[:, 0])
         b.receive(rrec, self.heur)
 
+    def _qstart(self):
+        """This rank's blocks' first local next_queue positions (nb + 1)."""
+        return np.concatenate([[0], np.cumsum(self._allb[self.c.rank])]).astype(np.int64)
+
+    def _rebalance_grouped_bc(self, st, all_n):
+        """Block-cyclic slices: the kept records go to the next beam's blocks as (parent, destination block) groups.
+        One count exchange carries, per destination rank, its blocks' (children, groups) and the children per (source
+        block, destination block); one all_to_all moves the segments; the receiver expands them in (its block, source
+        block, source) order — the global next_queue order within each block, which the stable score sort keeps for ties
+        (a score's ties never span two blocks) — with the senders' parent numbers mapped to global ranks."""
+        c, b = self.c, self.b
+        G, nb, me = c.world, self.nb, c.rank
+        D = G * nb
+        buf, cnt2 = b.pack_kept_grouped(all_n[me], ndig=D)            # (children, groups) per digit (rank, block)
+        sub = b.dest_subcounts(self._qstart(), D)                       # (nb source blocks, D digits)
+        send = torch.cat([cnt2.reshape(G, 2 * nb), sub.reshape(nb, G, nb).permute(1, 0, 2).reshape(G, nb * nb)], dim=1)
+        send2, recv2 = c.alltoall_counts_dev(send.contiguous())
+        send2 = np.asarray(send2, dtype=np.int64).reshape(G, 2 * nb + nb * nb)
+        recv2 = np.asarray(recv2, dtype=np.int64).reshape(G, 2 * nb + nb * nb)
+        sch, sgr = send2[:, 0:2 * nb:2], send2[:, 1:2 * nb:2]           # (dest rank, its block)
+        rch, rgr = recv2[:, 0:2 * nb:2], recv2[:, 1:2 * nb:2]           # (source, my block)
+        rsub = recv2[:, 2 * nb:].reshape(G, nb, nb)                      # (source, source block, my block)
+        ssz = (5 * sgr + (sch + 1) // 2).sum(axis=1)
+        rseg = 5 * rgr + (rch + 1) // 2                                  # u32 per (source, my block) segment
+        rsz = rseg.sum(axis=1)
+        self._mark(st, 'pack_kept')
+        so = np.concatenate([[0], np.cumsum(ssz)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(rsz)]).astype(np.int64)
+        rbuf = torch.empty(max(int(ro[-1]), 1), dtype=torch.int32, device=buf.device)
+        pieces = [buf[int(so[q]):int(so[q + 1])] if q != me else buf[:0] for q in range(G)]
+        outs = [rbuf[int(ro[q]):int(ro[q + 1])] if q != me else rbuf[:0] for q in range(G)]
+        c.alltoall_into(pieces, outs, what='kept records')
+        rbuf[int(ro[me]):int(ro[me + 1])].copy_(buf[int(so[me]):int(so[me + 1])])
+        self._mark(st, 'a2a_kept')
+        # segments (source q, my block p), source-major; children concatenated in that order
+        bases = ro[:-1, None] + np.concatenate([np.zeros((G, 1), np.int64), np.cumsum(rseg, axis=1)[:, :-1]], axis=1)
+        # target order (my block p, source block j, source q): run starts
+        cnt_pjq = rsub.transpose(2, 1, 0)                                # (p, j, q)
+        dst0 = np.concatenate([[0], np.cumsum(cnt_pjq.reshape(-1))])[:-1].reshape(nb, nb, G)
+        perm, src = [], 0   # (non-empty runs only: an empty run would share its start with the next one)
+        for q in range(G):
+            for p in range(nb):
+                for j in range(nb):
+                    if rsub[q, j, p]:
+                        perm.append((src, int(dst0[p, j, q])))
+                    src += int(rsub[q, j, p])
+        # the senders' parent numbers (rank-major over this turn's slices) -> global ranks, non-empty blocks
+        gstart, lstart = self.layout(self.turn)
+        voff = np.concatenate([[0], np.cumsum(self.counts[self.turn])])
+        bs = self.blocks[self.turn]
+        pmap = sorted((int(voff[r] + lstart[r, j]), int(gstart[r, j])) for r in range(G) for j in range(nb) if bs[r, j])
+        rrec = b.unpack_kept(rbuf, bases.reshape(-1), rgr.reshape(-1), rch.reshape(-1), perm=perm, pmap=pmap)
+        b.receive(rrec, self.heur)
+        self._bounds = [0] + np.cumsum(rch.sum(axis=0)).astype(np.int64).tolist()
+
     def _rebalance(self, st, all_n, K, dest_dev, oe, rec20):
         c, b = self.c, self.b
         rec = b.pack_kept(b.oe_n() if oe else all_n[c.rank], rec20=rec20)   # ahead of the counts
-        if c.world == 1:   # every kept record stays: K of them, known here (no round trip)
+        if c.world == 1 and self.bc:   # every kept record stays; its blocks' sizes are the next parts' bounds
+            dest_counts = dest_dev.cpu().numpy().astype(np.int64)
+            self._bounds = [0] + np.cumsum(dest_counts).tolist()
+            dest_counts = recv = np.array([int(dest_counts.sum())], dtype=np.int64)
+        elif c.world == 1:   # every kept record stays: K of them, known here (no round trip)
             dest_counts = recv = np.array([K], dtype=np.int64)
         else:
             dest_counts, recv = c.alltoall_counts_dev(dest_dev)
@@ -906,7 +1069,7 @@ class DistSolve:
         c.allreduce_tensor(rng, dist.ReduceOp.MIN)
         b.sel_begin(positions, rng)
         src = 0
-        for p in range(self.SEL_PASSES):
+        for p in range(self.SEL_PASSES + (len(positions) > 16)):   # 8-bit digits once more than 16 prefixes are live
             h = b.sel_hist(src)
             c.allreduce_tensor(h)
             b.sel_pick(h)
@@ -925,12 +1088,10 @@ class DistSolve:
         t, r = self.winner
         out = []
         while t >= 0:
-            cnt = self.counts[t]
-            offs = np.concatenate([[0], np.cumsum(cnt)])
-            owner = int(np.searchsorted(offs, r, side='right') - 1)
+            owner, loc = self.locate(t, r)
             vals = [0, 0, 0]
             if owner == self.c.rank:
-                lo, hi, par = self.b.turn_state(t, r - int(offs[owner]))
+                lo, hi, par = self.b.turn_state(t, loc)
                 vals = [_u64_to_i64(lo), _u64_to_i64(hi), par]
             lo, hi, par = self.c.broadcast_ints(vals, owner)
             out.append((lo & 0xFFFFFFFFFFFFFFFF, hi & 0xFFFFFFFFFFFFFFFF))
@@ -1083,7 +1244,7 @@ class HipBackend:
         lib.sbd_goal_table.argtypes = [vp, vp]
         lib.sbd_expand_launch.argtypes = [vp, i32]
         lib.sbd_expand_counts.argtypes = [vp, i32, vp, p64]
-        lib.sbd_expand_parts.argtypes = [vp, i32, i32, i64]
+        lib.sbd_expand_parts.argtypes = [vp, i32, i32, i64, vp]
         lib.sbd_part_counts.argtypes = [vp, i32, vp, p64]
         lib.sbd_part_pack.argtypes = [vp, i32, vp, i64]
         lib.sbd_set_claim_stream.argtypes = [vp, vp]
@@ -1096,6 +1257,12 @@ class HipBackend:
         lib.sbd_owner_claim.argtypes = [vp, vp, i64, i32, vp, vp, vp]
         lib.sbd_owner_finish.argtypes = [vp, vp]
         lib.sbd_owner_claim_all.argtypes = [vp, vp, i64, i32, vp, vp, vp]
+        lib.sbd_owner_claim_part.argtypes = [vp, i32, vp, i64, i64, i32, vp, vp, vp]
+        lib.sbd_block_counts.argtypes = [vp, i32, vp, vp]
+        lib.sbd_sel_eq_blocks.argtypes = [vp, i32, vp, vp]
+        lib.sbd_partition_blocks.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+        lib.sbd_dest_subcounts.argtypes = [vp, i32, vp, i32, vp]
+        lib.sbd_noise_fill_ranges.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_unpack_bits.argtypes = [vp, vp, i64, vp]
         lib.sbd_pack_bits_segs.argtypes = [vp, vp, i32, vp, vp, vp, vp]
@@ -1119,7 +1286,7 @@ class HipBackend:
         lib.sbd_partition_bfs.argtypes = [vp, u64, u64, i32, vp]
         lib.sbd_pack_kept.argtypes = [vp, vp, i32]
         lib.sbd_pack_kept_grouped.argtypes = [vp, vp, i64, vp]
-        lib.sbd_unpack_kept.argtypes = [vp, vp, i32, p64, p64, p64, vp]
+        lib.sbd_unpack_kept.argtypes = [vp, vp, i32, p64, p64, p64, vp, i32, vp, i32, vp]
         lib.sbd_receive.argtypes = [vp, vp, i64, i32]
         lib.sbd_mark_done.argtypes = [vp, i64]
         lib.sbd_mig_launch.argtypes = [vp, i32]
@@ -1194,13 +1361,18 @@ class HipBackend:
         return self.L.visited_capacity(self.h)
 
     # ---------------------------------------------------------------- step primitives
-    def expand_launch(self, world, n_global=0):
+    def expand_launch(self, world, n_global=0, bounds=None):
         """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait.
         world > 1: the pipelined key pass in self.parts exchange parts (n_global: the turn's parents over
-        all ranks, bounds what this rank receives)."""
+        all ranks, bounds what this rank receives; bounds: the parts' local parent bounds, block-cyclic slices)."""
         self.world_x = int(world)
         if self.parts and (world > 1 or self.KP1):
-            self._chk(self.lib.sbd_expand_parts(self.h, int(world), int(self.parts), int(n_global)), 'sbd_expand_parts')
+            bd = None
+            if bounds is not None:
+                bd = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64))
+                assert len(bd) == self.parts + 1
+            self._chk(self.lib.sbd_expand_parts(self.h, int(world), int(self.parts), int(n_global),
+                                                bd.ctypes.data if bd is not None else None), 'sbd_expand_parts')
             return
         self._chk(self.lib.sbd_expand_launch(self.h, int(world)), 'sbd_expand_launch')
 
@@ -1290,6 +1462,22 @@ class HipBackend:
                                                vs.ctypes.data, ps.ctypes.data, ret.data_ptr() if n_total else None),
                   'sbd_owner_claim_all')
 
+    def owner_claim_part(self, j, rbuf, v_begin, v_end, v_start, p_start, ret):
+        """Part j's records [v_begin, v_end) claimed in global order (on the claim stream: the caller's current one)."""
+        vs = np.ascontiguousarray(v_start, dtype=np.int64)
+        ps = np.ascontiguousarray(p_start, dtype=np.int64)
+        n = int(v_end) > int(v_begin)
+        self._chk(self.lib.sbd_owner_claim_part(self.h, int(j), rbuf.data_ptr() if n else None, int(v_begin), int(v_end),
+                                                len(vs), vs.ctypes.data, ps.ctypes.data, ret.data_ptr() if n else None),
+                  'sbd_owner_claim_part')
+
+    def block_counts(self, bounds):
+        """Survivors per local block (device int64, after apply)."""
+        bd = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64))
+        out = torch.zeros(len(bd) - 1, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_block_counts(self.h, len(bd) - 1, bd.ctypes.data, out.data_ptr()), 'sbd_block_counts')
+        return out
+
     def pack_bits(self, src, dst):
         """dst (ceil(n/8) bytes) <- the n answer bytes of src as bits (bit k of byte i = src[8i + k])."""
         if src.numel():
@@ -1352,6 +1540,15 @@ class HipBackend:
             self._chk(self.lib.sbd_noise_fill(self.h, len(acc0), wins.data_ptr(), acc0.ctypes.data, int(a), int(e)),
                       'sbd_noise_fill')
 
+    def noise_fill_ranges(self, wins, acc0, ranges):
+        """ranges: (a, b, dst) — draws [a, b) kept at ring positions dst.. (block-cyclic slices)."""
+        acc0 = np.ascontiguousarray(acc0, dtype=np.uint64)
+        if not len(acc0) or not ranges:
+            return
+        a, b, d = (np.ascontiguousarray([x[i] for x in ranges], dtype=np.uint64) for i in range(3))
+        self._chk(self.lib.sbd_noise_fill_ranges(self.h, len(acc0), wins.data_ptr(), acc0.ctypes.data, len(a),
+                                                 a.ctypes.data, b.ctypes.data, d.ctypes.data), 'sbd_noise_fill_ranges')
+
     def emit(self, k_off, N, off):
         self._chk(self.lib.sbd_emit(self.h, int(k_off), int(N), int(off)), 'sbd_emit')
 
@@ -1381,6 +1578,28 @@ class HipBackend:
         self._chk(self.lib.sbd_sel_eq(self.h, self.sel_eqbuf.data_ptr()), 'sbd_sel_eq')
         return self.sel_eqbuf
 
+    def sel_eq_blocks(self, qstart):
+        """The keep boundary's ties per local block (device int64, nb)."""
+        q = np.ascontiguousarray(np.asarray(qstart, dtype=np.int64))
+        out = torch.zeros(len(q) - 1, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_sel_eq_blocks(self.h, len(q) - 1, q.ctypes.data, out.data_ptr()), 'sbd_sel_eq_blocks')
+        return out
+
+    def partition_blocks(self, has_top, eq_all, rank, G, nb):
+        """Destinations (rank, block) of the kept records; per-digit counts (device int64, G * nb)."""
+        counts = torch.zeros(G * nb, dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_partition_blocks(self.h, int(bool(has_top)), eq_all.data_ptr() if eq_all is not None else None,
+                                                int(rank), int(G), int(nb), counts.data_ptr()), 'sbd_partition_blocks')
+        return counts
+
+    def dest_subcounts(self, qstart, D):
+        """Kept records per (local block, digit): device int64 (nb, D)."""
+        q = np.ascontiguousarray(np.asarray(qstart, dtype=np.int64))
+        out = torch.zeros((len(q) - 1) * int(D), dtype=torch.int64, device=self.device)
+        self._chk(self.lib.sbd_dest_subcounts(self.h, len(q) - 1, q.ctypes.data, int(D), out.data_ptr()),
+                  'sbd_dest_subcounts')
+        return out
+
     def partition(self, has_top, eq_all, rank, nsplit, G):
         """Kept records' destinations; per-destination counts as a device int64 tensor (no wait)."""
         counts = torch.zeros(G, dtype=torch.int64, device=self.device)
@@ -1394,26 +1613,32 @@ class HipBackend:
                   'sbd_partition_bfs')
         return counts
 
-    def pack_kept_grouped(self, n_rows):
+    def pack_kept_grouped(self, n_rows, ndig=None):
         """Grouped kept records (sbd_pack_kept_grouped): (int32 buffer of 22 bytes per local survivor, device
-        int64 (C_d, G_d) pairs per destination), enqueued before the counts reach the host."""
-        cap = 22 * int(n_rows) // 4 + 2 * self.world + 2
+        int64 (C_d, G_d) pairs per destination digit — ndig of them, default world), enqueued before the counts reach
+        the host."""
+        D = int(ndig or self.world)
+        cap = 22 * int(n_rows) // 4 + 2 * D + 2
         buf = torch.empty(max(cap, 1), dtype=torch.int32, device=self.device)
-        cnt2 = torch.zeros(2 * self.world, dtype=torch.int64, device=self.device)
+        cnt2 = torch.zeros(2 * D, dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_pack_kept_grouped(self.h, buf.data_ptr(), cap, cnt2.data_ptr()), 'sbd_pack_kept_grouped')
         return buf, cnt2
 
-    def unpack_kept(self, rbuf, bases, groups, children):
-        """The received groups (source segments at u32 offsets bases, in source order) as (n, 5) int32 records."""
+    def unpack_kept(self, rbuf, bases, groups, children, perm=None, pmap=None):
+        """The received groups (segments at u32 offsets bases, in order) as (n, 5) int32 records; perm: (source child,
+        destination record) run starts, pmap: (sender parent number, global rank) run starts (block-cyclic slices)."""
         n = int(np.sum(children))
         rec = torch.empty((max(n, 1), 5), dtype=torch.int32, device=self.device)
         b = np.ascontiguousarray(bases, dtype=np.int64)
         g = np.ascontiguousarray(groups, dtype=np.int64)
         c = np.ascontiguousarray(children, dtype=np.int64)
+        pm = np.ascontiguousarray(np.asarray(perm, dtype=np.int64).reshape(-1)) if perm else np.zeros(2, np.int64)
+        mp = np.ascontiguousarray(np.asarray(pmap, dtype=np.int64).reshape(-1)) if pmap else np.zeros(2, np.int64)
         P = self.C.POINTER(self.C.c_int64)
         self._chk(self.lib.sbd_unpack_kept(self.h, rbuf.data_ptr() if rbuf.numel() else None, len(b),
                                            b.ctypes.data_as(P), g.ctypes.data_as(P), c.ctypes.data_as(P),
-                                           rec.data_ptr()), 'sbd_unpack_kept')
+                                           rec.data_ptr(), len(perm) if perm else 0, pm.ctypes.data,
+                                           len(pmap) if pmap else 0, mp.ctypes.data), 'sbd_unpack_kept')
         return rec[:n]
 
     def pack_kept(self, n_rows, rec20=False):

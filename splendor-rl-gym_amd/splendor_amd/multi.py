@@ -54,14 +54,11 @@ def launch(spec: dict, gpus: int) -> dict:
 
 def _state_at(solve, t: int, r: int):
     """(lo, hi) of global queue position r of turn t; a collective (every rank calls it)."""
-    import numpy as np
-    cnt = solve.counts[t]
-    offs = np.concatenate([[0], np.cumsum(cnt)])
-    owner = int(np.searchsorted(offs, r, side='right') - 1)
+    owner, loc = solve.locate(t, r)   # (block-cyclic slices interleave the ranks)
     vals = [0, 0, 0]
     if owner == solve.c.rank:
         from .dist import _u64_to_i64
-        lo, hi, par = solve.b.turn_state(t, r - int(offs[owner]))
+        lo, hi, par = solve.b.turn_state(t, loc)
         vals = [_u64_to_i64(lo), _u64_to_i64(hi), par]
     lo, hi, _ = solve.c.broadcast_ints(vals, owner)
     return lo & 0xFFFFFFFFFFFFFFFF, hi & 0xFFFFFFFFFFFFFFFF

@@ -76,6 +76,7 @@ def _worker(rank, world, port, cfg, outdir):
         if cfg.get('deferred'):
             assert not comm.outstanding, f'step {len(trace)} left an all_to_all handle unwaited'
     out = {'trace': trace, 'counts': [c.tolist() for c in solve.counts], 'path': [list(x) for x in solve.path()],
+           'order': [solve.global_order(t) for t in range(len(solve.blocks))], 'bc': solve.bc,
            'slices': [[lo, hi, par] for lo, hi, par in b.turns],
            'mt': b.mt_state().tolist() if cfg['heur'] else None,
            'deferred': [comm.deferred_calls, comm.waits] if cfg.get('deferred') else None,
@@ -89,6 +90,11 @@ def _run(world, cfg):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
         return [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
+
+
+def assemble(res, t, i):
+    """Field i of turn t's queue in global order from the rank slices (block-cyclic slices: blocks j-major)."""
+    return sum((res[r]['slices'][t][i][a:a + n] for r, a, n in res[0]['order'][t]), [])
 
 
 CASES = [
@@ -168,6 +174,14 @@ CASES = [
          'small_cap': 8, 'deferred': True}),
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 9, 'heur': True, 'toggle': True, 'parts': 4,
          'goc': True}),
+    # block-cyclic slices (the default with global-order claims): 16 blocks per rank at world 3 and 4 (48 / 64
+    # boundaries: 8-bit select digits), one rank (the KP1 measurement's world-1 protocol), 20-byte records refuse them
+    (3, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 400, 'seed': 13, 'heur': True, 'parts': 16, 'goc': True}),
+    (4, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 500, 'seed': 14, 'heur': True, 'parts': 16, 'goc': True,
+         'deferred': True}),
+    (1, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 300, 'seed': 15, 'heur': True, 'parts': 4, 'goc': True}),
+    (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'goc': True,
+         'gkr': False}),
 ]
 
 
@@ -182,9 +196,7 @@ def test_sharded_solve_matches_oracle(world, cfg):
     assert [t['done'] for t in res[0]['trace']] == [t['done'] for t in trace]
     for t in range(o.nturns()):
         lo, hi, par, _ = o.turn_arrays(t)
-        glo = sum((r['slices'][t][0] for r in res), [])
-        ghi = sum((r['slices'][t][1] for r in res), [])
-        gpar = sum((r['slices'][t][2] for r in res), [])
+        glo, ghi, gpar = (assemble(res, t, i) for i in range(3))
         assert glo == lo.tolist() and ghi == hi.tolist(), f'turn {t}'
         if t > 0:
             assert gpar == par.tolist(), f'turn {t} parents'
@@ -200,6 +212,8 @@ def test_sharded_solve_matches_oracle(world, cfg):
         assert all(r['mt'] == o.mt_state().tolist() for r in res)
     if cfg.get('small_cap'):
         assert any(r['grown'] for r in res), 'no rank grew its receive bound'
+    if cfg.get('goc') and cfg['heur'] and cfg.get('parts', 0) >= 2:   # block-cyclic unless 20-byte records
+        assert res[0]['bc'] == (cfg.get('gkr', True) or world == 1), res[0]['bc']
     if cfg.get('deferred'):   # the deferred path really ran: every rank issued async exchanges and waited for each
         assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), [r['deferred'] for r in res]
     o.close()

@@ -80,10 +80,12 @@ def _free_port():
     return p
 
 
-def _digest_turn(outdir, t, world):
-    """sha256 digest of turn t's beam over the rank slices in rank order; the slices' files are removed."""
+def _digest_turn(outdir, t, world, order):
+    """sha256 digest of turn t's beam over the rank slices in global order (runs (rank, start, length): block-cyclic
+    slices interleave the ranks); the slices' files are removed."""
     fs = [os.path.join(outdir, f'keys_t{t}_r{r}.npy') for r in range(world)]
-    key = np.concatenate([np.load(f) for f in fs])
+    ks = [np.load(f) for f in fs]
+    key = np.concatenate([ks[r][a:a + n] for r, a, n in order])
     for f in fs:
         os.remove(f)
     return oracle_c.beam_digest(key), len(key)
@@ -131,11 +133,12 @@ def _worker(rank, world, port, cfg, outdir):
         if cfg.get('digest_inline'):   # wide beams: rank 0 digests each turn as it completes
             dist.barrier()
             if rank == 0:
-                st['digest'], st['beam'] = _digest_turn(outdir, len(trace), world)
+                st['digest'], st['beam'] = _digest_turn(outdir, len(trace), world, solve.global_order(len(trace)))
                 print(f'[world {world}] turn {len(trace)}: {st["n_parents"]} parents, digest {st["digest"]}',
                       flush=True)   # progress (pytest -s) for long runs
             dist.barrier()
-    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist(),
+    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'mt': b.mt_state().tolist(), 'bc': solve.bc,
+           'order': [solve.global_order(t) for t in range(len(solve.blocks))],
            'visited_capacity': list(b.visited_capacity()),
            'deferred': [comm.deferred_calls, comm.waits, comm.landings] if cfg.get('devdeferred') else None}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
@@ -169,7 +172,8 @@ def test_sharded_w4m_oracle_golden(world, name, backend, flags):
         for t, exp in enumerate(g['turns'], 1):
             a = turns[t - 1]
             assert (a['n_raw'], a['n_unique'], a['n_kept']) == (exp['n_raw'], exp['n_unique'], exp['n_kept']), t
-            key = np.concatenate([np.load(os.path.join(d, f'keys_t{t}_r{r}.npy')) for r in range(world)])
+            ks = [np.load(os.path.join(d, f'keys_t{t}_r{r}.npy')) for r in range(world)]
+            key = np.concatenate([ks[r][a:a + n] for r, a, n in res[0]['order'][t]])
             assert oracle_c.beam_digest(key) == exp['digest'], f'turn {t}'
     from splendor_amd.codec import state_key, decode, to_signed
     path = [to_signed(state_key(decode(lo, hi)[0], decode(lo, hi)[2])) for lo, hi in res[0]['path']]

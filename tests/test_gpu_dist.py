@@ -41,6 +41,8 @@ def _worker(rank, world, port, cfg, outdir):
         os.environ['SB_DIST_GKR'] = '1' if cfg['gkr'] else '0'
     if 'parts' in cfg:     # exchange parts of the pipelined key pass (default 4)
         os.environ['SB_DIST_PARTS'] = str(cfg['parts'])
+    if cfg.get('nobc'):    # contiguous rank ranges instead of block-cyclic slices
+        os.environ['SB_DIST_BC'] = '0'
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd'),
@@ -74,7 +76,8 @@ def _worker(rank, world, port, cfg, outdir):
         n = int(solve.counts[t][rank])
         rows = [b.turn_state(t, r) for r in range(n)]
         slices.append([[x[0] for x in rows], [x[1] for x in rows], [x[2] for x in rows]])
-    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'slices': slices,
+    out = {'trace': trace, 'path': [list(x) for x in solve.path()], 'slices': slices, 'bc': solve.bc,
+           'order': [solve.global_order(t) for t in range(len(solve.blocks))],
            'mt': b.mt_state().tolist(), 'visited': list(b.visited_capacity()),
            'deferred': [comm.deferred_calls, comm.waits, comm.landings] if cfg.get('devdeferred') else None}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
@@ -150,6 +153,16 @@ CASES = [
     (3, {'goal': 7, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 6, 'heur': True, 'chunks': 3, 'keypass': 0,
          'devdeferred': True}),
     (2, {'goal': 3, 'hid': 0, 'name': 'simple', 'width': 1, 'seed': 0, 'heur': False, 'devdeferred': True}),
+    # block-cyclic slices (the default of the key-owner protocol): each exchange part one block of the global queue,
+    # claimed as soon as it has arrived; 16 blocks per rank at world 3 (48 boundaries: 8-bit select digits), the RCCL
+    # contract at world 4, one rank in 4 blocks (the KP1 measurement), and the contiguous slices it replaces
+    (3, {'goal': 8, 'hid': 1, 'name': 'balanced', 'width': 20000, 'seed': 11, 'heur': True, 'parts': 16, 'bc': True}),
+    (4, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'devdeferred': True,
+         'bc': True}),
+    (1, {'goal': 8, 'hid': 2, 'name': 'aggressive', 'width': 40000, 'seed': 4, 'heur': True, 'kp1': True, 'ck': 1,
+         'bc': True}),
+    (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10, 'bc': True}),
+    (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'nobc': True, 'bc': False}),
 ]
 
 
@@ -164,12 +177,15 @@ def test_sharded_engine_matches_oracle(world, cfg):
                              beam_width=cfg['width'], mt_state625=st)
     trace = o.run()
     assert len(res[0]['trace']) == len(trace)
+    asm = lambda t, i: sum((res[r]['slices'][t][i][a:a + n] for r, a, n in res[0]['order'][t]), [])   # global order
     for t in range(o.nturns()):
         lo, hi, par, _ = o.turn_arrays(t)
-        assert sum((r['slices'][t][0] for r in res), []) == lo.tolist(), f'turn {t}'
-        assert sum((r['slices'][t][1] for r in res), []) == hi.tolist(), f'turn {t}'
+        assert asm(t, 0) == lo.tolist(), f'turn {t}'
+        assert asm(t, 1) == hi.tolist(), f'turn {t}'
         if t > 0:
-            assert sum((r['slices'][t][2] for r in res), []) == par.tolist(), f'turn {t} parents'
+            assert asm(t, 2) == par.tolist(), f'turn {t} parents'
+    if cfg.get('bc') is not None:
+        assert res[0]['bc'] == cfg['bc'], res[0]['bc']
     for a, b in zip(res[0]['trace'], trace):
         if not b['done']:
             assert (a['n_raw'], a['n_unique'], a['n_kept']) == (b['n_raw'], b['n_unique'], b['n_kept'])
