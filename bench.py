@@ -284,9 +284,12 @@ def run_single(args):
     win = Window(make, lambda e: e.step(), lambda e: e.sync(), lambda e: e.close(), first, length,
                  look=None if args.lookahead_edges else (lambda e, on: e.set_lookahead(on)))
 
+    vstats = []
+
     def phases(eng, turn0, seg):   # device phase times (HIP events recorded on the engine's stream)
         for i, p in enumerate(seg):
             p.update(eng.turn_times(turn0 + i))
+        vstats.append(eng.visited_stats())   # the visited set's growth record (shortened / skipped rebuilds)
 
     # the clock stops when every stream is idle: the MT producers' chunk that the segment's last step
     # launched for later turns is charged to the segment (--engine-stream-end: legacy accounting that
@@ -294,7 +297,18 @@ def run_single(args):
     per, elapsed, el_eng, segs = timed_steps(win, args.steps, args.warmup, lambda e: e.sync(), phases,
                                              sync_engine=lambda e: e.sync_engine(), engine_end=args.engine_stream_end)
     win.close()
-    return per, elapsed, el_eng, segs, (first, length, turns, win.engines)
+    return per, elapsed, el_eng, segs, (first, length, turns, win.engines), visited_summary(vstats)
+
+
+def visited_summary(vstats):
+    """The timed engines' visited sets: slots at the end, rebuilds, rebuilds short of the worst case or skipped (free
+    HBM ran short: a higher load and longer probe chains, never a different result), the peak load after a turn."""
+    if not vstats:
+        return None
+    return {'slots': max(v['slots'] for v in vstats), 'rebuilds': max(v['rebuilds'] for v in vstats),
+            'rebuilds_short': sum(v['rebuilds_short'] for v in vstats),
+            'rebuilds_skipped': sum(v['rebuilds_skipped'] for v in vstats),
+            'peak_load': max(v['peak_load'] for v in vstats)}
 
 
 def rexpand_bytes(n_parents, n_raw, n_unique):
@@ -350,9 +364,12 @@ def run_realistic(args):
     first, length, turns = probe_window(make, lambda e: e.step(), lambda e: e.close(), width)
     win = Window(make, lambda e: e.step(), sync, lambda e: e.close(), first, length)
 
+    vstats = []
+
     def phases(eng, turn0, seg):
         for i, p in enumerate(seg):
             p.update(eng.turn_times(turn0 + i))
+        vstats.append(eng.visited_stats())
 
     per, elapsed, _, segs = timed_steps(win, args.steps, args.warmup, sync, phases)
     win.close()
@@ -374,7 +391,8 @@ def run_realistic(args):
            'config': {'workload': f'realistic 2p goal_pts=15 --shuffle beam_width={width} (C4)', 'beam_width': width,
                       'b_raw': round(raw / parents, 3), 'b_uniq': round(uniq / parents, 3),
                       'segment_end': 'every stream', 'segments': segs,
-                      'warmup_engine': 'own (the timed steps start on fresh engines)'},
+                      'warmup_engine': 'own (the timed steps start on fresh engines)',
+                      'visited': visited_summary(vstats)},
            'phases_ms': ph,
            'roofline': {'bound': 'hbm', 'kernel': 'k_rexpand2', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 5),
@@ -438,7 +456,7 @@ def main():
         return bench_dist.main(args)
     if args.heuristic is None:
         args.heuristic = 'balanced'         # C3
-    per, elapsed, el_eng, segs, (first, length, turns, engines) = run_single(args)
+    per, elapsed, el_eng, segs, (first, length, turns, engines), vsum = run_single(args)
     parents = sum(p['n_parents'] for p in per)
     raw = sum(p['n_raw'] for p in per)
     uniq = sum(p['n_unique'] for p in per)
@@ -478,7 +496,8 @@ def main():
                                         if args.lookahead_edges else 'exactly the timed turns\' own'),
                    'segment_end': ('the engine stream (legacy: noise generated for later turns not waited for)'
                                    if args.engine_stream_end else 'every stream (noise generated in the segment charged to it)'),
-                   'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh engines)'},
+                   'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh engines)',
+                   'visited': vsum},
         'value_engine_stream_end': round(parents / el_eng, 1),
         'phases_ms': phases,
         'roofline': {'bound': 'hbm', 'kernel': dom.replace('ms_', 'k_'), 'achieved': round(achieved, 2),

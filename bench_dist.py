@@ -67,13 +67,36 @@ def sharded_pmc():
     return None
 
 
+def carried_n1(heuristic):
+    """The N>1 lines' same-workload reference: `bench.py --gpus 1 --heuristic H` (the single-GPU engine at 4M per GPU)
+    and the sharded protocol's world-1 run (SB_FORCE_DIST=1 SB_DIST_KP1=1: a rank's whole sharded device work on one
+    GPU, nothing exchanged), both measured on a GPU box and committed under profiles/ (the newest round's)."""
+    import glob
+    out = {}
+    for key, pat in (('single_gpu_engine', 'n1_{h}.json'), ('sharded_world1', 'n1_sharded_{h}.json')):
+        fs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r*',
+                                           pat.format(h=heuristic))))
+        if not fs:
+            continue
+        try:
+            d = json.load(open(fs[-1]))
+        except (OSError, ValueError):
+            continue
+        out[key] = {'value': d['value'], 'ms_per_step': d['ms_per_step'], 'n_gpus': 1,
+                    'source': os.path.relpath(fs[-1], os.path.dirname(os.path.abspath(__file__)))}
+    if out:
+        out['note'] = ('same workload (goal 15, -H ' + heuristic + ', 4M parents per GPU) on one MI355X, carried from the '
+                       'committed run; scaling_efficiency = value / (n_gpus x the single-GPU engine\'s value)')
+    return out or None
+
+
 def main(args):
     # RCCL prints its version banner on stdout at init: keep stdout for the one JSON line
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
     from bench import (GOAL, HBM_PEAK_GBS, METRIC, Window, cpu_baseline, expand_bytes, probe_window, step_bytes,
-                       timed_steps)
+                       timed_steps, visited_summary)
     from splendor_amd.dist import Comm, DistSolve, HipBackend, SerializedBackend, TimedProxy
     from splendor_amd.engine import HEURISTIC_IDS
     if 'RANK' not in os.environ:   # SB_FORCE_DIST=1 without a launcher: a world of one
@@ -98,6 +121,8 @@ def main(args):
     serial = os.environ.get('SB_DIST_SERIALIZE') == '1' and world > 1
     hostprof = {} if os.environ.get('SB_DIST_HOSTPROF') == '1' else None
 
+    bcs = []
+
     def make():
         random.seed(args.seed)
         b = HipBackend(rank=rank, world=world, device_index=dev, goal_pts=GOAL, use_heuristic=True,
@@ -111,9 +136,14 @@ def main(args):
             comm.devlock = b.lock
         if hostprof is not None:   # host time inside each backend / collective call (SB_DIST_HOSTPROF=1)
             b, comm = TimedProxy(b, hostprof), TimedProxy(comm, hostprof)
-        return DistSolve(b, comm, goal_pts=GOAL, use_heuristic=True, beam_width=W)
+        s = DistSolve(b, comm, goal_pts=GOAL, use_heuristic=True, beam_width=W)
+        bcs.append(s.bc)
+        return s
+
+    vstats = []
 
     def close(s):
+        vstats.append(s.b.visited_stats())   # this rank's owner shard: rebuilds short / skipped, peak load
         s.b.close()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()   # the exchange buffers of this solve go back to the device
@@ -174,7 +204,10 @@ def main(args):
                                             if args.lookahead_edges else 'exactly the timed turns\' own'),
                        'segment_end': ('the engine stream (legacy: noise rounds for later turns not waited for)'
                                        if args.engine_stream_end else 'every stream + barrier'),
-                       'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh solves)'},
+                       'segments': segs, 'warmup_engine': 'own (the timed steps start on fresh solves)',
+                       'slices': ('block-cyclic: the next beam dealt in world x parts blocks, claims per part on arrival'
+                                  if bcs and bcs[-1] else 'contiguous rank ranges'),
+                       'visited_rank0': visited_summary(vstats[1:] or vstats)},
             'value_engine_stream_end': round(parents / el_eng_max, 1),
             # bytes rank 0 sent to other ranks per timed step, by exchange (Comm.acct; RCCL's own traffic)
             'exchange_MB_per_step_rank0': {k: round(sum(p.get('xbytes', {}).get(k, 0) for p in per) / len(per) / 1e6, 2)
@@ -217,6 +250,12 @@ def main(args):
                 out['roofline']['traffic'] = sh['hbm_bytes_per_launch']
                 out['roofline']['traffic_kernel'] = sh['kernel']
                 out['roofline']['traffic_source'] = sh['source']
+        if world > 1:   # the same workload on one GPU, measured on a GPU box and carried
+            n1 = carried_n1(args.heuristic)
+            if n1:
+                out['n1_same_workload'] = n1
+                if n1.get('single_gpu_engine'):
+                    out['scaling_efficiency'] = round(out['value'] / (world * n1['single_gpu_engine']['value']), 4)
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only, after the timed region
             out['cpu_baseline'] = cpu_baseline(args.width, args.heuristic, args.seed, first)
         elif world > 1:

@@ -163,6 +163,11 @@ int sb_visited_size(sb_engine* e, uint64_t* out);
  * could pass 60% load, the table is rehashed into 2^k times the slots while free HBM allows; results
  * do not depend on the capacity.  Sharded mode: this rank's owner shard. */
 int sb_visited_capacity(sb_engine* e, uint64_t* capacity, int32_t* rebuilds);
+/* out6 = [slots, rebuilds, rebuilds smaller than the turn's worst case wanted (free HBM ran short), rebuilds wanted and
+ * not made, peak load after a turn (keys / slots, ppm), keys] of the visited set (sharded: this rank's owner shard).
+ * A shortened or skipped growth raises the load (longer probe chains) without changing a result; the HARD_LOAD (85%)
+ * check after a turn is the limit.  SB_DEBUG_VISITED_MAX=<slots> (tests) fails rebuilds above it. */
+int sb_visited_stats(sb_engine* e, uint64_t* out6);
 
 void sb_destroy(sb_engine* e);
 const char* sb_last_error(void);
@@ -236,6 +241,11 @@ int sbd_expand_counts(sb_engine* e, int32_t nchunk, int64_t* chunk_owner_counts,
 int sbd_expand_parts(sb_engine* e, int32_t world, int32_t nparts, int64_t n_global, const int64_t* bounds);
 int sbd_part_counts(sb_engine* e, int32_t part, int64_t* owner_counts, int64_t* recv_capacity);
 int sbd_part_pack(sb_engine* e, int32_t part, uint64_t* d_key, int64_t send_base);
+/* global-order claims (flags bit 11): sbd_expand_parts packs every part right behind its key pass into the engine's
+ * send buffer (part j's owner groups at its first raw slot = the earlier parts' records); sbd_part_pack then only
+ * registers send_base (d_key must be null) and the caller sends views of *d_ptr (*cap u64, valid until the next
+ * expansion).  Claim segments may read this rank's own records there (p_start with bit 63 set). */
+int sbd_send_buffer(sb_engine* e, void** d_ptr, int64_t* cap);
 int sbd_set_claim_stream(sb_engine* e, void* stream);
 int sbd_owner_total(sb_engine* e, int64_t n_total);
 /* the turn's received records will exceed the receive bound sbd_part_counts reported (an estimate from the raw
@@ -261,9 +271,11 @@ int sbd_owner_claim(sb_engine* e, const uint64_t* d_key, int64_t n, int32_t nseg
 int sbd_owner_finish(sb_engine* e, uint8_t* d_ret);
 /* global-order claims (flags bit 11): after every part has arrived, the turn's n_total records in one pass, in
  * virtual (source rank, part, record) order — the global (parent rank, ordinal) order; segment k = virtual records
- * [v_start[k], v_start[k+1]) (the last to n_total) found at d_key + p_start[k].  d_ret[v] = 1 for a first occurrence,
- * final after sbd_owner_finish.  The own children are records to this rank itself (sbd_part_counts / sbd_part_pack
- * include them). */
+ * [v_start[k], v_start[k+1]) (the last to n_total) found at d_key + p_start[k].  d_ret[v] = 1 for a claim that inserted
+ * or took its key — NOT final in this mode: a record displaced by a later claim keeps 1 and only its lost bit (engine
+ * state) says so.  The answers are final only as packed by sbd_pack_bits_segs, which folds the lost bits in;
+ * sbd_owner_finish does nothing here and sbd_pack_bits refuses the mode (SB_ERR_STATE).  The own children are records
+ * to this rank itself (sbd_part_counts / sbd_part_pack include them). */
 int sbd_owner_claim_all(sb_engine* e, const uint64_t* d_key, int64_t n_total, int32_t nseg, const int64_t* v_start,
                         const int64_t* p_start, uint8_t* d_ret);
 /* global-order claims of one exchange part as soon as it has arrived (block-cyclic slices, or world 1: part j of every

@@ -926,6 +926,11 @@ struct Engine {
     // visited-set growth (grow_table): largest raw children per parent seen so far, tables rebuilt
     double raw_ratio = 32.0;
     int n_grow = 0;
+    // growth that fell short (ranks sharing one GPU's HBM can leave less than the sizing saw): a
+    // table rebuilt smaller than the turn's worst case wanted, a rebuild wanted and none made; the peak load (keys /
+    // slots after a turn) — all reported by sb_visited_stats and the bench lines, never silent
+    int n_grow_short = 0, n_grow_skip = 0;
+    double peak_load = 0.0;
     uint64_t own_visited = 1;             // sharded: keys held by this owner shard (root counted at every rank)
     bool records = true;                  // sharded: this turn made records for other owners (world > 1)
     int64_t rec_per_parent = MAX_CHILDREN;   // sharded record slots per parent (flags bit 5: 48, overflow checked)
@@ -946,6 +951,7 @@ struct Engine {
     bool kept20 = false;                  // this turn's kept records are 20 bytes (sbd_pack_kept rec20)
     DBuf<uint64_t> goc_seg;               // their segment table (v start, physical start)
     uint64_t* h_goc = nullptr;            // pinned staging of it
+    hipEvent_t goc_ev = nullptr;          // ... recorded after its copy (the next turn's rewrite waits for that only)
     int ks_parts = 0;
     int64_t ks_c[17] = {};
     int64_t ks_pb[17] = {};               // each part's first local parent (ks_pb[ks_parts] = n): chunk c of part j holds
@@ -953,13 +959,12 @@ struct Engine {
     bool ks_bounds = false;               // this turn's parts came from the caller's bounds (block-cyclic slices)
     size_t ks_ccoff[17] = {};
     uint64_t ks_sbase[17] = {};           // each part's first index in the turn's send buffers (sbd_part_pack)
-    struct KpTab* h_kt = nullptr;         // pinned: the apply's answer-place table (global-order claims)
-    DBuf<uint64_t> d_kt;
     hipEvent_t ks_ev[16] = {};
     uint32_t* h_pc = nullptr;             // pinned: per part, per owner record counts (16 x 64)
     uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
     hipStream_t s_claim = nullptr;
     DBuf<uint32_t> ks_rdr, ks_sown, ks_cc, ks_tot, ks_pc;
+    DBuf<uint64_t> ks_send;               // global-order claims: the turn's packed records (sbd_send_buffer)
     // card-set ownership of the sharded dedup (sb_mig.inc, cfg flags bit 8): range side (parents' owner digits,
     // their rows' send positions, the partition histogram, per-owner counts), expand side (the received parents
     // as SoA + global ranks, raw counts / offsets), gmap (global rank -> expand index | first received record),
@@ -994,25 +999,38 @@ constexpr double GROW_LOAD = 0.6;
 constexpr double HARD_LOAD = 0.85;
 constexpr size_t GROW_RESERVE = (size_t)4 << 30;
 
+// SB_DEBUG_VISITED_MAX=<slots> (tests): a visited-set rebuild above it fails as if the HBM were taken
+static bool debug_visited_allows(uint64_t slots) {
+    const char* lim = std::getenv("SB_DEBUG_VISITED_MAX");
+    return !lim || (double)slots <= std::strtod(lim, nullptr);
+}
+
 static void grow_table(Engine& E, Entry*& tab, uint64_t& mask, double projected) {
     const uint64_t cap = mask + 1;
     uint64_t ncap = cap;
     const double grow_load = (E.cfg.flags & 16) ? 0.25 : GROW_LOAD;   // flags bit 4 (test): eager growth
     while (projected > grow_load * (double)ncap && ncap < (1ull << 36)) ncap <<= 1;
     if (ncap == cap) return;
+    const uint64_t want = ncap;
     size_t freeb = 0, totalb = 0;
     SB_HIP(hipMemGetInfo(&freeb, &totalb));
     while (ncap > cap && ncap * sizeof(Entry) + GROW_RESERVE > freeb) ncap >>= 1;
-    if (ncap == cap) return;
     // Another process on the GPU (ranks sharing it) may take HBM between the sizing and the allocation: then a
-    // smaller table, or none — growth is ahead of need, and the HARD_LOAD check after the turn is the limit
+    // smaller table, or none — growth is ahead of need, and the HARD_LOAD check after the turn is the limit.  Either
+    // is counted (n_grow_short, n_grow_skip: sb_visited_stats)
     Entry* nt = nullptr;
     for (; ncap > cap; ncap >>= 1) {
-        if (debug_hbm_allows(ncap * sizeof(Entry)) && hipMalloc((void**)&nt, ncap * sizeof(Entry)) == hipSuccess) break;
+        if (debug_visited_allows(ncap) && debug_hbm_allows(ncap * sizeof(Entry)) &&
+            hipMalloc((void**)&nt, ncap * sizeof(Entry)) == hipSuccess)
+            break;
         (void)hipGetLastError();
         nt = nullptr;
     }
-    if (!nt) return;
+    if (!nt) {
+        E.n_grow_skip++;
+        return;
+    }
+    if (ncap < want) E.n_grow_short++;
     SB_HIP(hipMemsetAsync(nt, 0xFF, ncap * sizeof(Entry), E.s));
     hipLaunchKernelGGL(k_rehash, dim3(grid_cap((int64_t)std::min<uint64_t>(cap, 1ull << 40), 256, 1u << 16)), dim3(256), 0,
                        E.s, tab, cap, nt, ncap - 1, E.d_small + 1);
@@ -1278,6 +1296,7 @@ static void engine_step(Engine& E, sb_step_stats* out) {
     out->n_raw = (int64_t)*E.h_nraw;
     out->n_unique = nu;
     E.visited += (uint64_t)nu;
+    E.peak_load = std::max(E.peak_load, (double)E.visited / (double)(E.tab_mask + 1));
     if (n > 0) E.raw_ratio = std::max(E.raw_ratio, (double)out->n_raw / (double)n);
     if ((double)E.visited > HARD_LOAD * (double)(E.tab_mask + 1))
         throw HipError{hipErrorOutOfMemory, "visited set above 85% load and no larger table fits in free HBM"};
@@ -1819,6 +1838,18 @@ int sb_visited_size(sb_engine* h, uint64_t* out) {
     return SB_OK;
 }
 
+int sb_visited_stats(sb_engine* h, uint64_t* out6) {
+    if (!h || !out6) return SB_ERR_ARG;
+    const Engine& E = h->E;
+    out6[0] = (E.own ? E.own_mask : E.tab_mask) + 1;
+    out6[1] = (uint64_t)E.n_grow;
+    out6[2] = (uint64_t)E.n_grow_short;
+    out6[3] = (uint64_t)E.n_grow_skip;
+    out6[4] = (uint64_t)(E.peak_load * 1e6 + 0.5);   // ppm
+    out6[5] = E.own ? E.own_visited : E.visited;
+    return SB_OK;
+}
+
 int sb_visited_capacity(sb_engine* h, uint64_t* capacity, int32_t* rebuilds) {
     if (!h || !capacity || !rebuilds) return SB_ERR_ARG;
     const Engine& E = h->E;
@@ -1913,8 +1944,7 @@ void sb_destroy(sb_engine* h) {
         if (e) (void)hipEventDestroy(e);
     if (E.h_pc) (void)hipHostFree(E.h_pc);
     if (E.h_goc) (void)hipHostFree(E.h_goc);
-    if (E.h_kt) (void)hipHostFree(E.h_kt);
-    E.d_kt.release();
+    if (E.goc_ev) (void)hipEventDestroy(E.goc_ev);
     E.goc_seg.release();
     for (auto& e : E.ks_ev)
         if (e) (void)hipEventDestroy(e);

@@ -32,9 +32,9 @@ SB_HEUR_HOST = 15   # a Python HEURISTICS callable scores next_queue on the host
 POW_EXPONENTS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 1.2, 2.0, 2.5, 2.8, 3.2)
 POW_BASES = 256
 EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_read_next', 'sb_prune', 'sb_turn_times', 'sb_num_turns', 'sb_turn_size', 'sb_read_turn', 'sb_path',
-            'sb_get_mt_state', 'sb_sync', 'sb_set_lookahead', 'sb_sync_engine', 'sb_visited_size', 'sb_visited_capacity', 'sb_destroy', 'sb_last_error', 'sb_version', 'sb_build_id',
+            'sb_get_mt_state', 'sb_sync', 'sb_set_lookahead', 'sb_sync_engine', 'sb_visited_size', 'sb_visited_capacity', 'sb_visited_stats', 'sb_destroy', 'sb_last_error', 'sb_version', 'sb_build_id',
             'sb_debug_successors', 'sb_debug_alloc', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk', 'sb_debug_topk_scores', 'sb_debug_expand_bench', 'sb_debug_oe_merge',
-            'sbd_goal_table', 'sbd_expand_launch', 'sbd_expand_counts', 'sbd_expand_parts', 'sbd_part_counts', 'sbd_part_pack', 'sbd_set_claim_stream', 'sbd_owner_total', 'sbd_grow_receive', 'sbd_expand_defer', 'sbd_raw_total', 'sbd_pack', 'sbd_owner_begin', 'sbd_owner_claim', 'sbd_owner_finish', 'sbd_owner_claim_all', 'sbd_owner_claim_part', 'sbd_pack_bits', 'sbd_unpack_bits', 'sbd_pack_bits_segs', 'sbd_unpack_bits_segs', 'sbd_apply', 'sbd_apply_finish', 'sbd_emit',
+            'sbd_goal_table', 'sbd_expand_launch', 'sbd_expand_counts', 'sbd_expand_parts', 'sbd_part_counts', 'sbd_part_pack', 'sbd_send_buffer', 'sbd_set_claim_stream', 'sbd_owner_total', 'sbd_grow_receive', 'sbd_expand_defer', 'sbd_raw_total', 'sbd_pack', 'sbd_owner_begin', 'sbd_owner_claim', 'sbd_owner_finish', 'sbd_owner_claim_all', 'sbd_owner_claim_part', 'sbd_pack_bits', 'sbd_unpack_bits', 'sbd_pack_bits_segs', 'sbd_unpack_bits_segs', 'sbd_apply', 'sbd_apply_finish', 'sbd_emit',
             'sbd_key_range', 'sbd_sel_begin', 'sbd_sel_hist', 'sbd_sel_pick', 'sbd_sel_compact', 'sbd_sel_eq', 'sbd_set_stream', 'sbd_noise_info', 'sbd_noise_chunk', 'sbd_noise_sync', 'sbd_noise_pack', 'sbd_noise_fill', 'sbd_noise_fill_ranges', 'sbd_partition', 'sbd_partition_bfs', 'sbd_block_counts', 'sbd_sel_eq_blocks', 'sbd_partition_blocks', 'sbd_dest_subcounts', 'sbd_pack_kept', 'sbd_pack_kept_grouped', 'sbd_unpack_kept', 'sbd_receive', 'sbd_mark_done',
             'sbd_mig_launch', 'sbd_mig_counts', 'sbd_mig_pack', 'sbd_mig_expand', 'sbd_mig_claim', 'sbd_mig_apply', 'sbd_mig_place', 'sbd_keypass_ms',
             'sbd_oe_pack', 'sbd_oe_counts', 'sbd_oe_emit', 'sbd_oe_ties', 'sbd_oe_tie_read', 'sbd_oe_partition',
@@ -142,6 +142,7 @@ def lib():
         L.sb_get_mt_state.argtypes = [vp, u32p]
         L.sb_visited_size.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.sb_visited_capacity.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
+        L.sb_visited_stats.argtypes = [vp, vp]
         L.sb_sync.argtypes = [vp]
         L.sb_set_lookahead.argtypes = [vp, C.c_int32]
         L.sb_sync_engine.argtypes = [vp]
@@ -166,6 +167,16 @@ def visited_capacity(h) -> tuple[int, int]:
     cap, n = C.c_uint64(), C.c_int32()
     check(lib().sb_visited_capacity(h, C.byref(cap), C.byref(n)), 'sb_visited_capacity')
     return cap.value, n.value
+
+
+def visited_stats(h) -> dict:
+    """The visited set's growth record (sb_visited_stats): slots, rebuilds, rebuilds that fell short of the turn's worst
+    case (free HBM), rebuilds wanted and not made, the peak load after a turn, keys."""
+    import numpy as np
+    out = np.zeros(6, np.uint64)
+    check(lib().sb_visited_stats(h, out.ctypes.data), 'sb_visited_stats')
+    return {'slots': int(out[0]), 'rebuilds': int(out[1]), 'rebuilds_short': int(out[2]), 'rebuilds_skipped': int(out[3]),
+            'peak_load': round(int(out[4]) * 1e-6, 6), 'keys': int(out[5])}
 
 
 def check(rc: int, what: str = ''):

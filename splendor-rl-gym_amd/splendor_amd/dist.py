@@ -53,6 +53,81 @@ GKR = os.environ.get('SB_DIST_GKR', '1') != '0'
 # SB_DIST_BC=0: contiguous rank ranges (claims after the last part)
 BC = os.environ.get('SB_DIST_BC', '1') != '0'
 
+class ShmMeta:
+    """Host all_gather of small int64 vectors among the ranks of one node through shared memory (the step's metadata:
+    the turn sync, each exchange part's per-owner counts).  gloo's TCP ring took 170 us at world 2 and 6 ms at world 8
+    on an 8-core host (profiles/gloo_latency.py); here a rank writes its vector into its slot, then its round number,
+    and reads every slot once every rank's number has reached the round: a few microseconds plus the ranks' skew.
+
+    Slots alternate by round parity: a rank writing round k + 1 knows every rank finished reading round k - 1 (each
+    published round k only after that).  Ordering: x86-64 keeps stores in order and loads in order (TSO), so the data
+    a rank stores before its round number is visible to any rank that sees the number."""
+
+    SLOT = 1024   # int64 per rank and slot (the turn sync is 257 + parts)
+    TIMEOUT_S = 600.0
+
+    def __init__(self, rank, world, group):
+        from multiprocessing import shared_memory
+        import platform
+        if platform.machine() not in ('x86_64', 'AMD64'):
+            raise RuntimeError('ShmMeta relies on x86-64 store/load ordering')
+        self.rank, self.world = rank, world
+        nbytes = 8 * (world * 8 + 2 * world * self.SLOT)
+        name = [None]
+        if rank == 0:
+            self._shm = shared_memory.SharedMemory(create=True, size=nbytes)
+            self._shm.buf[:nbytes] = bytes(nbytes)
+            name[0] = self._shm.name
+        dist.broadcast_object_list(name, src=0, group=group)
+        if rank != 0:   # attach without registering: the creator owns (and unlinks) the segment
+            from multiprocessing import resource_tracker
+            reg = resource_tracker.register
+            resource_tracker.register = lambda *a, **k: None
+            try:
+                self._shm = shared_memory.SharedMemory(name=name[0])
+            finally:
+                resource_tracker.register = reg
+        a = np.ndarray((world * 8 + 2 * world * self.SLOT,), dtype=np.int64, buffer=self._shm.buf)
+        self.seq = a[:world * 8].reshape(world, 8)   # [r, 0]: the last round rank r published (a line per rank)
+        self.data = a[world * 8:].reshape(2, world, self.SLOT)
+        self.round = 0
+        dist.barrier(group=group)   # every rank attached before the creator may unlink
+        if rank == 0:
+            self._shm.unlink()       # the mapping lives on in every process; nothing left under /dev/shm
+
+    def allgather(self, arr: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(arr, dtype=np.int64)
+        if len(a) > self.SLOT:
+            raise ValueError(f'ShmMeta: {len(a)} values exceed the slot ({self.SLOT})')
+        self.round += 1
+        k = self.round
+        slot = self.data[k & 1]
+        slot[self.rank, :len(a)] = a
+        self.seq[self.rank, 0] = k
+        spins, t0 = 0, None
+        while int(self.seq[:, 0].min()) < k:
+            spins += 1
+            if spins > 64:
+                os.sched_yield()
+                if spins % 4096 == 0:   # a rank that died would leave the others spinning
+                    t0 = t0 or time.monotonic()
+                    if time.monotonic() - t0 > self.TIMEOUT_S:
+                        raise RuntimeError(f'ShmMeta: round {k} incomplete after {self.TIMEOUT_S} s '
+                                           f'(rounds seen: {self.seq[:, 0].tolist()})')
+        return slot[:, :len(a)].copy()
+
+    def close(self):
+        try:
+            self.seq = self.data = None
+            self._shm.close()
+        except Exception:
+            pass
+
+
+# host metadata over shared memory when every rank is on this node (SB_DIST_SHM=0: the gloo group)
+SHM = os.environ.get('SB_DIST_SHM', '1') != '0'
+
+
 class Comm:
     """torch.distributed helpers; gloo works on CPU tensors (device tensors are staged)."""
 
@@ -65,6 +140,14 @@ class Comm:
         # host-side metadata (the turn sync: slice sizes + goal tables) goes over a gloo group: it runs
         # while the expansion occupies every CU, which a device collective would have to wait for
         self.meta = dist.new_group(backend='gloo') if self.world > 1 else None
+        # ... and, when every rank runs on this node (one process per GPU of one MI355X node), over shared memory
+        self.shm = None
+        local = int(os.environ.get('LOCAL_WORLD_SIZE', self.world))
+        if self.world > 1 and SHM and local == self.world:
+            try:
+                self.shm = ShmMeta(self.rank, self.world, self.meta)
+            except (RuntimeError, OSError):
+                self.shm = None
         self.devlock = None   # profiling (SerializedBackend.lock): gloo's staging copies under the device lock
         self.xbytes = {}      # bytes this rank sent to other ranks, per exchange (DistSolve.step hands them out)
 
@@ -197,6 +280,8 @@ class Comm:
         if self.world == 1:   # nothing to exchange: no device round trip
             return a.reshape(1, len(a))
         if host:
+            if self.shm is not None and len(a) <= ShmMeta.SLOT:
+                return self.shm.allgather(a)
             t = torch.from_numpy(a)
             out = [torch.empty_like(t) for _ in range(self.world)]
             dist.all_gather(out, t, group=self.meta)
@@ -719,13 +804,14 @@ class DistSolve:
                 pieces = [key[int(ostart[o]):int(ostart[o + 1])] if o != me else key[:0] for o in range(W)]
                 _, hd = c.alltoall_pieces(pieces, remote, what='records', out=rbuf[ans_base:ans_base + rtot])
                 handles.append(hd)
-                if cnt[me]:
+                if cnt[me] and not bc:
                     rbuf[ans_base + rtot:need].copy_(key[int(ostart[me]):int(ostart[me + 1])])
-                if bc:   # block-cyclic: part j is the global order's next range — claim it now, sources in order
+                if bc:   # block-cyclic: part j is the global order's next range — claim it now, sources in order; this
+                    # rank's own records are read where they were packed (bit 63: the send buffer), not copied
                     vs, ps, v = [], [], ans_base
                     for q in range(W):
                         vs.append(v)
-                        ps.append(ans_base + (rtot if q == me else int(remote[:q].sum())))
+                        ps.append(send_base + int(ostart[me]) - (1 << 63) if q == me else ans_base + int(remote[:q].sum()))
                         v += int(from_src[q])
                     c.wait(hd)                                # RCCL: the claim stream waits for the part's transfer
                     handles[-1] = None
@@ -1165,6 +1251,15 @@ class TimedProxy:
         return call
 
 
+class _DevArray:
+    """Engine-owned device memory as a torch tensor (__cuda_array_interface__, no copy): the packed records the
+    expansion wrote, sent by the all_to_all straight from where they are."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {'shape': (int(n),), 'typestr': '<i8', 'data': (int(ptr or 0), False),
+                                         'version': 2, 'strides': None}
+
+
 class HipBackend:
     """Per-rank primitives on the MI355X engine (libsplendor_beam.so, sbd_* entry points).
 
@@ -1247,6 +1342,7 @@ class HipBackend:
         lib.sbd_expand_parts.argtypes = [vp, i32, i32, i64, vp]
         lib.sbd_part_counts.argtypes = [vp, i32, vp, p64]
         lib.sbd_part_pack.argtypes = [vp, i32, vp, i64]
+        lib.sbd_send_buffer.argtypes = [vp, vp, p64]
         lib.sbd_set_claim_stream.argtypes = [vp, vp]
         lib.sbd_owner_total.argtypes = [vp, i64]
         lib.sbd_grow_receive.argtypes = [vp, i64, p64]
@@ -1360,6 +1456,10 @@ class HipBackend:
         """(slots, rebuilds) of this rank's owner shard of the visited set."""
         return self.L.visited_capacity(self.h)
 
+    def visited_stats(self) -> dict:
+        """Growth record of this rank's owner shard (sb_visited_stats)."""
+        return self.L.visited_stats(self.h)
+
     # ---------------------------------------------------------------- step primitives
     def expand_launch(self, world, n_global=0, bounds=None):
         """Enqueue this turn's expansion (own children claimed, records for the other owners); no wait.
@@ -1389,7 +1489,15 @@ class HipBackend:
 
     def part_pack(self, j, n, send_base):
         """Part j's n records in owner groups (on the claim stream: the caller's current stream); with card-set
-        ownership each record is 12 bytes (key, global parent rank << 7 | move), 3n int32."""
+        ownership each record is 12 bytes (key, global parent rank << 7 | move), 3n int32.  Global-order claims: packed
+        by the expansion itself into the engine's send buffer — a view of it at send_base."""
+        if self.goc:
+            self._chk(self.lib.sbd_part_pack(self.h, int(j), None, int(send_base)), 'sbd_part_pack')
+            if j == 0 or getattr(self, '_send_t', None) is None:
+                ptr, cap = self.C.c_void_p(), self.C.c_int64()
+                self._chk(self.lib.sbd_send_buffer(self.h, self.C.byref(ptr), self.C.byref(cap)), 'sbd_send_buffer')
+                self._send_t = torch.as_tensor(_DevArray(ptr.value, cap.value), device=self.device)
+            return self._send_t[int(send_base):int(send_base) + int(n)]
         if self.mig:   # 12-byte records, three int32 each
             key = self._empty(max(3 * int(n), 1), torch.int32)[:3 * int(n)]
         else:

@@ -142,6 +142,10 @@ class BeamEngine:
         """(slots, rebuilds): the visited set grows between turns (include/splendor_beam.h)."""
         return L.visited_capacity(self._h)
 
+    def visited_stats(self) -> dict:
+        """Growth record of the visited set (sb_visited_stats): rebuilds short of the worst case or skipped, peak load."""
+        return L.visited_stats(self._h)
+
 
 def device_successors(lo, hi, device: int = 0):
     """Ordered successors of a batch of packed states on the GPU (the k_expand enumeration)."""

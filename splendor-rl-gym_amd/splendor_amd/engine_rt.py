@@ -113,6 +113,9 @@ class RealisticEngine:
         """(slots, rebuilds) of the visited set (grown between turns)."""
         return L.visited_capacity(self._h)
 
+    def visited_stats(self) -> dict:
+        return L.visited_stats(self._h)
+
     def mt_state(self):
         out = np.zeros(625, np.uint32)
         L.check(L.lib().sb_get_mt_state(self._h, out))

@@ -63,3 +63,25 @@ def test_realistic_growth_vs_oracle():
     assert rebuilds >= 2 and cap > 1024, (cap, rebuilds)
     eng.close()
     o.close()
+
+
+def test_growth_short_and_skipped_are_counted(monkeypatch):
+    """A rebuild the HBM cannot hold is shortened or skipped (ranks sharing one GPU can take the memory between the
+    sizing and the allocation: gpurun_out/r5final3); both are counted and the peak load reported
+    (sb_visited_stats), and the results stay the oracle's.  SB_DEBUG_VISITED_MAX caps rebuilds at 4096 slots: on this
+    solve (goal 2, simple, W=150 from 1024 slots) a turn's worst case wants 8192 and gets 4096 (short), a later one
+    wants more and gets none (skipped); its keys end at about 0.73 of the 4096 slots."""
+    monkeypatch.setenv('SB_DEBUG_VISITED_MAX', '4096')
+    random.seed(21)
+    st = random.getstate()[1]
+    eng = BeamEngine(goal_pts=2, use_heuristic=True, heuristic=HEURISTIC_IDS['simple'], beam_width=150,
+                     mt_state625=st, visited_log2=10)
+    ora = oracle_c.OracleSolve(2, use_heuristic=True, heuristic_name='simple', beam_width=150, mt_state625=st)
+    _stepwise(eng, ora)
+    assert eng.path() == ora.path()
+    vs = eng.visited_stats()
+    assert vs['slots'] == 4096 and vs['rebuilds'] >= 1, vs
+    assert vs['rebuilds_short'] >= 1 and vs['rebuilds_skipped'] >= 1, vs
+    assert 0.5 < vs['peak_load'] <= 0.85 and vs['keys'] == eng.visited_size(), vs
+    eng.close()
+    ora.close()
