@@ -12,7 +12,14 @@ latency per collective round.  The records travel in P parts beside the key pass
 is done, so what the claims wait for beyond the key pass is max(x / P, x - kp (P - 1) / P) for a transfer time x
 and key pass kp (round 5: the last part's transfer always counts — earlier rounds counted only max(0, x - kp)).
 Every other exchange counts in full.
+Round 6: the latency is two terms.  Host metadata rounds (the turn sync and each part's counts: 1 +
+parts per step, host all_gathers) at --host-lat-us, measured on CPU by profiles/gloo_latency.py (shared memory, the
+default since round 6: 8 us a round at world 8; gloo's TCP ring: 1.3-6 ms on an 8-core host) — the JSON it wrote can be
+given as --host-lat-json.  Device collective rounds (RCCL: the select's 8 all_reduces, the tie and count gathers, the
+parts' and the answers' all_to_alls, the kept records' counts and segments: ~20 per step, counted from SB_DIST_HOSTPROF
+in profiles/r6/) at --lat-us, which stays an assumption: one GPU per box here.
     python3 profiles/project_n8.py TABLE.json BENCH.json [--B 250,400,600] [--lat-us 30] [--rounds 20]
+                                   [--host-lat-json profiles/r6/gloo_latency_w8_container.json | --host-lat-us 8]
 """
 import argparse
 import json
@@ -26,7 +33,10 @@ def main():
     ap.add_argument('bench')
     ap.add_argument('--B', default='250,400,600', help='effective all_to_all GB/s per GPU')
     ap.add_argument('--lat-us', type=float, default=30.0, help='latency per collective round (us)')
-    ap.add_argument('--rounds', type=int, default=20, help='collective rounds per step on the critical path')
+    ap.add_argument('--rounds', type=int, default=20, help='device collective rounds per step on the critical path')
+    ap.add_argument('--host-lat-us', type=float, default=None, help='host metadata all_gather latency (us)')
+    ap.add_argument('--host-lat-json', default=None, help='profiles/gloo_latency.py output: its shared-memory chain')
+    ap.add_argument('--host-gloo', action='store_true', help='with --host-lat-json: the gloo chain instead')
     ap.add_argument('--single-ms', type=float, default=4.548, help='one GPU ms/step (BENCH_r04: 4.548)')
     ap.add_argument('--balanced-kept', action='store_true',
                     help='kept records as if every rank sent 7/8 of W x 32 B (a protocol whose kept records are produced '
@@ -37,6 +47,11 @@ def main():
                     help='device time per rank and step from another measurement (e.g. the world-1 key-pass run, '
                          'profiles/busy_union.py) instead of the table\'s serialised total')
     a = ap.parse_args()
+    host_lat = a.host_lat_us
+    if a.host_lat_json:
+        hj = json.load(open(a.host_lat_json))
+        host_lat = hj['part_counts_chain_us_max_rank' if a.host_gloo else 'shm_part_counts_chain_us_max_rank']
+    host_rounds = 1 + a.parts
     t = json.load(open(a.table))
     b = [json.loads(l) for l in open(a.bench) if l.startswith('{')][-1]
     mean = t.get('robust_mean_ms', t['mean_ms'])   # launches that waited on another rank's work capped
@@ -47,13 +62,18 @@ def main():
         x['kept records'] = a.W * 32 * 7 / 8 / 1e6
     print(f'device per rank (serialised world-{t["world"]} traces, mean of ranks): {dev:.3f} ms; key pass {keypass:.3f} ms')
     print('exchange per rank and step (MB sent to other ranks):', {k: round(v, 1) for k, v in x.items()})
-    out = {'device_ms': dev, 'exchange_MB': x, 'projection': []}
+    out = {'device_ms': dev, 'exchange_MB': x, 'projection': [],
+           'latency_model': {'device_rounds': a.rounds, 'device_lat_us': a.lat_us, 'host_rounds': host_rounds,
+                             'host_lat_us': host_lat}}
+    if host_lat is not None:
+        print(f'latency: {a.rounds} device collective rounds x {a.lat_us} us (assumed) + {host_rounds} host metadata rounds '
+              f'x {host_lat} us (measured)')
     for B in [float(v) for v in a.B.split(',')]:
         crit = sum(v for k, v in x.items() if k not in OVERLAPPED) / B          # MB / (GB/s) = ms
         over = sum(v for k, v in x.items() if k in OVERLAPPED) / B
         P = a.parts
         exposed_rec = max(over / P, over - keypass * (P - 1) / P) if over > 0 else 0.0
-        lat = a.rounds * a.lat_us / 1e3
+        lat = a.rounds * a.lat_us / 1e3 + (host_rounds * host_lat / 1e3 if host_lat is not None else 0.0)
         step = dev + crit + exposed_rec + lat
         gps = 8 * a.W / (step * 1e-3) / 1e9
         row = {'B_GBps': B, 'critical_exchange_ms': round(crit, 3), 'records_exposed_ms': round(exposed_rec, 3),

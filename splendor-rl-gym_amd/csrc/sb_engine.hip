@@ -937,6 +937,7 @@ struct Engine {
     size_t rcap_turn = 0;                 // sharded: record slots of the expansion in flight
     bool apply_pending = false;           // sharded: sbd_apply done, sbd_apply_finish not yet
     bool expand_pending = false;          // sharded: sbd_expand_launch done, sbd_expand_counts not yet
+    bool goal_copied = false;             // sharded: the slice's goal table is on its way to h_small (event ev[0])
     bool raw_pending = false;             // sharded world 1: sbd_expand_defer done, sbd_raw_total not yet
     int expand_world = 1;
     uint64_t own_pending = 0;             // sharded: children this rank may have claimed in its expansion (bound)
