@@ -342,6 +342,11 @@ int sbd_noise_fill_ranges(sb_engine* e, int32_t m, const void* wins, const uint6
  * keep boundary's ties. */
 int sbd_key_range(sb_engine* e, void* range_dev);
 int sbd_sel_begin(sb_engine* e, int32_t npos, const int64_t* positions, const void* range_dev);
+/* the same with positions nexact.. as block boundaries (block-cyclic slices): each stops refining once its bucket holds at
+ * most fmax keys over all ranks — its boundary is then the bucket's lowest key (a block ends between scores, any
+ * boundary keeps the global order) — so the later passes resolve the keep boundary alone */
+int sbd_sel_begin_approx(sb_engine* e, int32_t npos, const int64_t* positions, const void* range_dev, int32_t nexact,
+                         int64_t fmax);
 int sbd_sel_hist(sb_engine* e, int32_t src, void* hist_dev);
 int sbd_sel_pick(sb_engine* e, void* hist_dev);   /* also clears hist_dev for the next pass */
 int sbd_sel_compact(sb_engine* e);
@@ -364,7 +369,8 @@ int sbd_partition_bfs(sb_engine* e, uint64_t k_off, uint64_t n_total, int32_t wo
 int sbd_block_counts(sb_engine* e, int32_t nblk, const int64_t* bounds, void* out_dev);
 int sbd_sel_eq_blocks(sb_engine* e, int32_t nblk, const int64_t* qstart, void* eq_dev);
 int sbd_partition_blocks(sb_engine* e, int32_t has_top, const void* eq_all_dev, int32_t rank, int32_t world, int32_t nblk,
-                         void* dest_counts_dev);
+                         void* dest_counts_dev, const int64_t* qstart, void* sub_dev);   /* qstart / sub_dev (nullable):
+                         sbd_dest_subcounts' counts written on the way (nblk x world * nblk int64) */
 int sbd_dest_subcounts(sb_engine* e, int32_t nblk, const int64_t* qstart, int32_t D, void* out_dev);
 /* kept records grouped by destination, next_queue order inside a group, one all_to_all buffer of at least the
  * kept count (the local next_queue size always suffices, so it can be enqueued before the counts reach the host).

@@ -35,7 +35,7 @@ EXPORTED = ('sb_init_tables', 'sb_create', 'sb_step', 'sb_read_next', 'sb_prune'
             'sb_get_mt_state', 'sb_sync', 'sb_set_lookahead', 'sb_sync_engine', 'sb_visited_size', 'sb_visited_capacity', 'sb_visited_stats', 'sb_destroy', 'sb_last_error', 'sb_version', 'sb_build_id',
             'sb_debug_successors', 'sb_debug_alloc', 'sb_debug_mt_words', 'sb_debug_mt_words_cfg', 'sb_debug_scores', 'sb_debug_topk', 'sb_debug_topk_scores', 'sb_debug_expand_bench', 'sb_debug_oe_merge',
             'sbd_goal_table', 'sbd_expand_launch', 'sbd_expand_counts', 'sbd_expand_parts', 'sbd_part_counts', 'sbd_part_pack', 'sbd_send_buffer', 'sbd_set_claim_stream', 'sbd_owner_total', 'sbd_grow_receive', 'sbd_expand_defer', 'sbd_raw_total', 'sbd_pack', 'sbd_owner_begin', 'sbd_owner_claim', 'sbd_owner_finish', 'sbd_owner_claim_all', 'sbd_owner_claim_part', 'sbd_pack_bits', 'sbd_unpack_bits', 'sbd_pack_bits_segs', 'sbd_unpack_bits_segs', 'sbd_apply', 'sbd_apply_finish', 'sbd_emit',
-            'sbd_key_range', 'sbd_sel_begin', 'sbd_sel_hist', 'sbd_sel_pick', 'sbd_sel_compact', 'sbd_sel_eq', 'sbd_set_stream', 'sbd_noise_info', 'sbd_noise_chunk', 'sbd_noise_sync', 'sbd_noise_pack', 'sbd_noise_fill', 'sbd_noise_fill_ranges', 'sbd_partition', 'sbd_partition_bfs', 'sbd_block_counts', 'sbd_sel_eq_blocks', 'sbd_partition_blocks', 'sbd_dest_subcounts', 'sbd_pack_kept', 'sbd_pack_kept_grouped', 'sbd_unpack_kept', 'sbd_receive', 'sbd_mark_done',
+            'sbd_key_range', 'sbd_sel_begin', 'sbd_sel_begin_approx', 'sbd_sel_hist', 'sbd_sel_pick', 'sbd_sel_compact', 'sbd_sel_eq', 'sbd_set_stream', 'sbd_noise_info', 'sbd_noise_chunk', 'sbd_noise_sync', 'sbd_noise_pack', 'sbd_noise_fill', 'sbd_noise_fill_ranges', 'sbd_partition', 'sbd_partition_bfs', 'sbd_block_counts', 'sbd_sel_eq_blocks', 'sbd_partition_blocks', 'sbd_dest_subcounts', 'sbd_pack_kept', 'sbd_pack_kept_grouped', 'sbd_unpack_kept', 'sbd_receive', 'sbd_mark_done',
             'sbd_mig_launch', 'sbd_mig_counts', 'sbd_mig_pack', 'sbd_mig_expand', 'sbd_mig_claim', 'sbd_mig_apply', 'sbd_mig_place', 'sbd_keypass_ms',
             'sbd_oe_pack', 'sbd_oe_counts', 'sbd_oe_emit', 'sbd_oe_ties', 'sbd_oe_tie_read', 'sbd_oe_partition',
             'sbd_oe_partition_bfs', 'sbd_oe_segments',

@@ -802,7 +802,10 @@ class DistSolve:
             with ctx():
                 key = b.part_pack(j, int(ostart[-1]), send_base)
                 pieces = [key[int(ostart[o]):int(ostart[o + 1])] if o != me else key[:0] for o in range(W)]
-                _, hd = c.alltoall_pieces(pieces, remote, what='records', out=rbuf[ans_base:ans_base + rtot])
+                if W > 1:
+                    _, hd = c.alltoall_pieces(pieces, remote, what='records', out=rbuf[ans_base:ans_base + rtot])
+                else:    # one rank (the KP1 measurement): nothing leaves, no collective to order after
+                    hd = None
                 handles.append(hd)
                 if cnt[me] and not bc:
                     rbuf[ans_base + rtot:need].copy_(key[int(ostart[me]):int(ostart[me + 1])])
@@ -988,7 +991,9 @@ class DistSolve:
             pos = ([self.W] if has_top else []) + [max(1, -(-j * K // nsp)) for j in range(1, nsp)]
             eq_all = None
             if pos:
-                self._multiselect(pos, st)
+                # block-cyclic: the block boundaries stop refining once their bucket holds <= 1/16 of a block
+                approx = (int(has_top), max(1, K // (nsp * 16))) if self.bc else None
+                self._multiselect(pos, st, approx)
                 self._mark(st, 'sel_passes')
                 if has_top and oe:   # ties at the keep boundary in next_queue order: by position, over all ranks
                     tp, need = b.oe_ties()
@@ -1002,7 +1007,7 @@ class DistSolve:
             if oe:
                 dest_dev = b.oe_partition(has_top, pstar if has_top else -1, len(pos) - int(has_top), G)
             elif self.bc:
-                dest_dev = b.partition_blocks(has_top, eq_all, c.rank, G, self.nb)
+                dest_dev = b.partition_blocks(has_top, eq_all, c.rank, G, self.nb, qstart=self._qstart())
             else:
                 dest_dev = b.partition(has_top, eq_all, c.rank, len(pos) - int(has_top), G)
         elif oe:
@@ -1143,7 +1148,7 @@ class DistSolve:
 
     SEL_PASSES = 7   # ceil(64 / 10): passes after the last digit are no-ops on the device
 
-    def _multiselect(self, positions, st=None):
+    def _multiselect(self, positions, st=None, approx=None):
         """Global key at each 1-based position of the (score desc) order and how many of its ties
         precede the position, left in the backend's select state: MSB radix select over 10-bit
         digits below the bits common to every key (all_reduce(MIN) of the encoded range); per pass
@@ -1153,7 +1158,10 @@ class DistSolve:
         c, b = self.c, self.b
         rng = b.key_range()
         c.allreduce_tensor(rng, dist.ReduceOp.MIN)
-        b.sel_begin(positions, rng)
+        if approx is not None:   # (positions approx[0].. are block boundaries, frozen at <= approx[1] keys a bucket)
+            b.sel_begin_approx(positions, rng, *approx)
+        else:
+            b.sel_begin(positions, rng)
         src = 0
         for p in range(self.SEL_PASSES + (len(positions) > 16)):   # 8-bit digits once more than 16 prefixes are live
             h = b.sel_hist(src)
@@ -1288,6 +1296,7 @@ class HipBackend:
     # measurement aid: the world > 1 key-owner path (pipelined key pass, global-order claims) at world 1, so one
     # GPU runs a rank's whole sharded device work with its streams overlapping as on an 8-GPU node (no exchange)
     KP1 = os.environ.get('SB_DIST_KP1') == '1'
+    PRIO = os.environ.get('SB_DIST_PRIO', '1') == '1'   # A/B (profiles/r6/s6): world-1 key-pass run 8.04-8.09 -> 7.86-7.93 ms
 
     def __init__(self, *, rank: int, world: int, device_index: int, goal_pts: int, use_heuristic: bool,
                  heuristic: int, beam_width: int, mt_state625, root=(0, 0), visited_log2: int = 0,
@@ -1320,7 +1329,9 @@ class HipBackend:
         self.h = h
         self.world = world
         # one stream for the engine's kernels and the collectives: ordered without host syncs
-        self.stream = torch.cuda.Stream(self.device)
+        # SB_DIST_PRIO=1: the engine stream (key passes, packs, the step's short kernels) at high priority over the claim
+        # stream, whose persistent claim grid would otherwise hold back the engine's single-workgroup scans
+        self.stream = torch.cuda.Stream(self.device, priority=-1 if self.PRIO else 0)
         torch.cuda.set_stream(self.stream)
         L.check(self.lib.sbd_set_stream(self.h, C.c_void_p(self.stream.cuda_stream)), 'sbd_set_stream')
         # world > 1: the pipelined key pass; received records are claimed on a second stream beside it
@@ -1356,7 +1367,7 @@ class HipBackend:
         lib.sbd_owner_claim_part.argtypes = [vp, i32, vp, i64, i64, i32, vp, vp, vp]
         lib.sbd_block_counts.argtypes = [vp, i32, vp, vp]
         lib.sbd_sel_eq_blocks.argtypes = [vp, i32, vp, vp]
-        lib.sbd_partition_blocks.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+        lib.sbd_partition_blocks.argtypes = [vp, i32, vp, i32, i32, i32, vp, vp, vp]
         lib.sbd_dest_subcounts.argtypes = [vp, i32, vp, i32, vp]
         lib.sbd_noise_fill_ranges.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
         lib.sbd_pack_bits.argtypes = [vp, vp, i64, vp]
@@ -1368,6 +1379,7 @@ class HipBackend:
         lib.sbd_emit.argtypes = [vp, u64, u64, i64]
         lib.sbd_key_range.argtypes = [vp, vp]
         lib.sbd_sel_begin.argtypes = [vp, i32, vp, vp]
+        lib.sbd_sel_begin_approx.argtypes = [vp, i32, vp, vp, i32, i64]
         lib.sbd_sel_hist.argtypes = [vp, i32, vp]
         lib.sbd_sel_pick.argtypes = [vp, vp]
         lib.sbd_sel_compact.argtypes = [vp]
@@ -1672,6 +1684,12 @@ class HipBackend:
         p = np.ascontiguousarray(np.array(pos, dtype=np.int64))
         self._chk(self.lib.sbd_sel_begin(self.h, len(pos), p.ctypes.data, rng.data_ptr()), 'sbd_sel_begin')
 
+    def sel_begin_approx(self, pos, rng, nexact, fmax):
+        self.sel_begin(pos, rng)   # (the histogram buffers)
+        p = np.ascontiguousarray(np.array(pos, dtype=np.int64))
+        self._chk(self.lib.sbd_sel_begin_approx(self.h, len(pos), p.ctypes.data, rng.data_ptr(), int(nexact), int(fmax)),
+                  'sbd_sel_begin_approx')
+
     def sel_hist(self, src):
         self._chk(self.lib.sbd_sel_hist(self.h, int(src), self.sel_h.data_ptr()), 'sbd_sel_hist')
         return self.sel_h
@@ -1693,15 +1711,23 @@ class HipBackend:
         self._chk(self.lib.sbd_sel_eq_blocks(self.h, len(q) - 1, q.ctypes.data, out.data_ptr()), 'sbd_sel_eq_blocks')
         return out
 
-    def partition_blocks(self, has_top, eq_all, rank, G, nb):
-        """Destinations (rank, block) of the kept records; per-digit counts (device int64, G * nb)."""
+    def partition_blocks(self, has_top, eq_all, rank, G, nb, qstart=None):
+        """Destinations (rank, block) of the kept records; per-digit counts (device int64, G * nb).  qstart (the blocks'
+        local next_queue starts): the kept records per (local block, digit) are counted on the way (dest_subcounts)."""
         counts = torch.zeros(G * nb, dtype=torch.int64, device=self.device)
+        q = np.ascontiguousarray(np.asarray(qstart, dtype=np.int64)) if qstart is not None else None
+        self._sub = torch.empty(nb * G * nb, dtype=torch.int64, device=self.device) if q is not None else None
         self._chk(self.lib.sbd_partition_blocks(self.h, int(bool(has_top)), eq_all.data_ptr() if eq_all is not None else None,
-                                                int(rank), int(G), int(nb), counts.data_ptr()), 'sbd_partition_blocks')
+                                                int(rank), int(G), int(nb), counts.data_ptr(),
+                                                q.ctypes.data if q is not None else None,
+                                                self._sub.data_ptr() if q is not None else None), 'sbd_partition_blocks')
         return counts
 
     def dest_subcounts(self, qstart, D):
-        """Kept records per (local block, digit): device int64 (nb, D)."""
+        """Kept records per (local block, digit): device int64 (nb, D) — counted by partition_blocks when it had them."""
+        if getattr(self, '_sub', None) is not None:
+            sub, self._sub = self._sub, None
+            return sub
         q = np.ascontiguousarray(np.asarray(qstart, dtype=np.int64))
         out = torch.zeros((len(q) - 1) * int(D), dtype=torch.int64, device=self.device)
         self._chk(self.lib.sbd_dest_subcounts(self.h, len(q) - 1, q.ctypes.data, int(D), out.data_ptr()),
