@@ -961,6 +961,7 @@ struct Engine {
     size_t ks_ccoff[17] = {};
     uint64_t ks_sbase[17] = {};           // each part's first index in the turn's send buffers (sbd_part_pack)
     hipEvent_t ks_ev[16] = {};
+    bool goc_tk_clear = false;            // sbd_expand_parts cleared the parts' claim tickets for this turn
     uint32_t* h_pc = nullptr;             // pinned: per part, per owner record counts (16 x 64)
     uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
     hipStream_t s_claim = nullptr;

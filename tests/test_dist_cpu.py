@@ -8,7 +8,6 @@ reference primitives.
 import json
 import os
 import random
-import socket
 import tempfile
 
 import numpy as np
@@ -16,14 +15,6 @@ import pytest
 import torch.multiprocessing as mp
 
 import oracle_c
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _worker(rank, world, port, cfg, outdir):
@@ -42,9 +33,8 @@ def _worker(rank, world, port, cfg, outdir):
     import torch.distributed as dist
     from dist_ref_backend import RefBackend
     from splendor_amd.dist import Comm, DistSolve
-    os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(port)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    # a file store in the test's directory: no TCP port to pick and lose to a parallel test worker before binding
+    dist.init_process_group('gloo', init_method='file://' + os.path.join(outdir, 'store'), rank=rank, world_size=world)
     random.seed(cfg['seed'])
     st = random.getstate()[1]
     b = RefBackend(rank, heuristic=cfg['hid'], mt_state625=st, world=world)
@@ -88,7 +78,7 @@ def _worker(rank, world, port, cfg, outdir):
 
 def _run(world, cfg):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), cfg, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, None, cfg, d), nprocs=world, join=True)
         return [json.load(open(os.path.join(d, f'rank{r}.json'))) for r in range(world)]
 
 
