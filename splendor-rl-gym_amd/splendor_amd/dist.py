@@ -124,6 +124,9 @@ class ShmMeta:
             pass
 
 
+# block-cyclic slices: part 0's blocks of the next beam, relative to the other parts' (SB_DIST_P0)
+P0 = float(os.environ.get('SB_DIST_P0', '1.0'))
+
 # host metadata over shared memory when every rank is on this node (SB_DIST_SHM=0: the gloo group)
 SHM = os.environ.get('SB_DIST_SHM', '1') != '0'
 
@@ -964,8 +967,6 @@ class DistSolve:
     def _post_dedup(self, st, all_n, off):
         """noise, emission, joint select, rebalance and receive of a step (after the dedup exchange)."""
         c, b = self.c, self.b
-        if getattr(b, 'timing', False):   # device time of this step's key kernels (the bench's world > 1 roofline)
-            st['keypass_ms'] = b.keypass_ms()
         k_off = int(all_n[:c.rank].sum())
         N = int(all_n.sum())
         st['n_unique'] = N
@@ -988,7 +989,13 @@ class DistSolve:
         if self.heur:
             has_top = N > self.W
             nsp = G * self.nb   # destination ranges: the ranks, or (block-cyclic) the next beam's world x parts blocks
-            pos = ([self.W] if has_top else []) + [max(1, -(-j * K // nsp)) for j in range(1, nsp)]
+            if self.bc and P0 != 1.0 and self.nb > 1:   # part 0's blocks P0 times the others': its key pass, which the
+                # claims wait for, is shorter (any boundaries are valid, the same on every rank)
+                wt = np.where(np.arange(nsp) < G, P0, 1.0)
+                cw = np.cumsum(wt)[:-1] / wt.sum()
+                pos = ([self.W] if has_top else []) + [max(1, int(np.ceil(K * x))) for x in cw]
+            else:
+                pos = ([self.W] if has_top else []) + [max(1, -(-j * K // nsp)) for j in range(1, nsp)]
             eq_all = None
             if pos:
                 # block-cyclic: the block boundaries stop refining once their bucket holds <= 1/16 of a block
@@ -1027,6 +1034,8 @@ class DistSolve:
             self._rebalance(st, all_n, K, dest_dev, oe, rec20)
         if self.heur:
             self.noise.background()
+        if getattr(b, 'timing', False):   # device time of this step's key kernels (the bench's world > 1 roofline), read
+            st['keypass_ms'] = b.keypass_ms()   # here, long done, not on the way from the apply to the emission
         if self.lookahead:
             self._launch_front(K)   # the next turn's expansion (K parents in all) overlaps its goal check
         else:   # a benchmark's window edge (bench.py): the next step() launches it

@@ -20,6 +20,8 @@ import oracle_c
 def _worker(rank, world, port, cfg, outdir):
     if 'gkr' in cfg:   # grouped kept records on the rebalance's wire (dist.GKR, read at import)
         os.environ['SB_DIST_GKR'] = '1' if cfg['gkr'] else '0'
+    if 'p0' in cfg:   # block-cyclic: part 0's blocks relative to the others' (dist.P0, read at import)
+        os.environ['SB_DIST_P0'] = str(cfg['p0'])
     if 'chunks' in cfg:
         os.environ['SB_DIST_CHUNKS'] = str(cfg['chunks'])
         os.environ['SB_DIST_CHUNK_MIN'] = '0'
@@ -172,6 +174,11 @@ CASES = [
     (1, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 300, 'seed': 15, 'heur': True, 'parts': 4, 'goc': True}),
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'goc': True,
          'gkr': False}),
+    # part 0's blocks a third / twice the others' (SB_DIST_P0): any boundaries, the same on every rank
+    (3, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 400, 'seed': 13, 'heur': True, 'parts': 4, 'goc': True,
+         'p0': 0.33}),
+    (2, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 300, 'seed': 14, 'heur': True, 'parts': 3, 'goc': True,
+         'p0': 2.0, 'deferred': True}),
 ]
 
 
