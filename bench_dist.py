@@ -212,6 +212,11 @@ def main(args):
             # bytes rank 0 sent to other ranks per timed step, by exchange (Comm.acct; RCCL's own traffic)
             'exchange_MB_per_step_rank0': {k: round(sum(p.get('xbytes', {}).get(k, 0) for p in per) / len(per) / 1e6, 2)
                                            for k in sorted({k for p in per for k in p.get('xbytes', {})})},
+            # collectives rank 0 issued per timed step: device-group rounds (RCCL's latency terms) and host metadata
+            # all_gathers (shared memory on one node) — counted by Comm, not assumed
+            'collectives_per_step_rank0': {
+                'device': round(sum(p.get('collectives', (0, 0))[0] for p in per) / len(per), 2),
+                'host': round(sum(p.get('collectives', (0, 0))[1] for p in per) / len(per), 2)},
             'roofline': {'bound': 'hbm', 'kernel': 'whole step (per GPU, SURVEY §8d byte model)',
                          'achieved': round(gbs / world, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(gbs / world / HBM_PEAK_GBS, 5), 'traffic': None},

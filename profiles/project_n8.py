@@ -33,7 +33,8 @@ def main():
     ap.add_argument('bench')
     ap.add_argument('--B', default='250,400,600', help='effective all_to_all GB/s per GPU')
     ap.add_argument('--lat-us', type=float, default=30.0, help='latency per collective round (us)')
-    ap.add_argument('--rounds', type=int, default=20, help='device collective rounds per step on the critical path')
+    ap.add_argument('--rounds', type=float, default=None, help='device collective rounds per step on the critical path '
+                    '(default: the bench line\'s counted collectives_per_step_rank0, else 20)')
     ap.add_argument('--host-lat-us', type=float, default=None, help='host metadata all_gather latency (us)')
     ap.add_argument('--host-lat-json', default=None, help='profiles/gloo_latency.py output: its shared-memory chain')
     ap.add_argument('--host-gloo', action='store_true', help='with --host-lat-json: the gloo chain instead')
@@ -54,6 +55,12 @@ def main():
     host_rounds = 1 + a.parts
     t = json.load(open(a.table))
     b = [json.loads(l) for l in open(a.bench) if l.startswith('{')][-1]
+    counted = b.get('collectives_per_step_rank0')
+    rounds_src = 'assumed'
+    if a.rounds is None and counted:   # counted by Comm in the traced run
+        a.rounds, host_rounds, rounds_src = counted['device'], counted['host'], 'counted'
+    elif a.rounds is None:
+        a.rounds = 20
     mean = t.get('robust_mean_ms', t['mean_ms'])   # launches that waited on another rank's work capped
     dev = mean['device total (engine stream)'] if a.device_ms is None else a.device_ms
     keypass = mean.get('expand', 0.0)
@@ -63,11 +70,12 @@ def main():
     print(f'device per rank (serialised world-{t["world"]} traces, mean of ranks): {dev:.3f} ms; key pass {keypass:.3f} ms')
     print('exchange per rank and step (MB sent to other ranks):', {k: round(v, 1) for k, v in x.items()})
     out = {'device_ms': dev, 'exchange_MB': x, 'projection': [],
-           'latency_model': {'device_rounds': a.rounds, 'device_lat_us': a.lat_us, 'host_rounds': host_rounds,
+           'latency_model': {'device_rounds': a.rounds, 'rounds_source': rounds_src, 'device_lat_us': a.lat_us,
+                             'host_rounds': host_rounds,
                              'host_lat_us': host_lat}}
     if host_lat is not None:
-        print(f'latency: {a.rounds} device collective rounds x {a.lat_us} us (assumed) + {host_rounds} host metadata rounds '
-              f'x {host_lat} us (measured)')
+        print(f'latency: {a.rounds} device collective rounds ({rounds_src}) x {a.lat_us} us (assumed) + {host_rounds} host '
+              f'metadata rounds x {host_lat} us (measured)')
     for B in [float(v) for v in a.B.split(',')]:
         crit = sum(v for k, v in x.items() if k not in OVERLAPPED) / B          # MB / (GB/s) = ms
         over = sum(v for k, v in x.items() if k in OVERLAPPED) / B

@@ -153,6 +153,8 @@ class Comm:
                 self.shm = None
         self.devlock = None   # profiling (SerializedBackend.lock): gloo's staging copies under the device lock
         self.xbytes = {}      # bytes this rank sent to other ranks, per exchange (DistSolve.step hands them out)
+        self.ncoll = 0        # device-group collectives issued (the step's latency rounds; DistSolve.step resets them)
+        self.nhost = 0        # host metadata all_gathers (shared memory or the gloo group)
 
     def acct(self, what, nbytes):
         self.xbytes[what] = self.xbytes.get(what, 0) + int(nbytes)
@@ -178,6 +180,7 @@ class Comm:
 
     def allreduce(self, arr: np.ndarray, op) -> np.ndarray:
         t = self._to(self._cp(lambda: torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64)).to(self.device)))
+        self.ncoll += 1
         dist.all_reduce(t, op=op)
         return t.cpu().numpy()
 
@@ -188,6 +191,7 @@ class Comm:
         if self.world == 1:
             return s
         out = torch.empty(self.world * s.numel(), dtype=s.dtype, device=s.device)
+        self.ncoll += 1
         dist.all_gather_into_tensor(out, s)
         return out
 
@@ -208,6 +212,7 @@ class Comm:
             return c, c
         send = self._to(counts.reshape(-1))   # world x k counts: k per destination (equal splits)
         recv = torch.empty_like(send)
+        self.ncoll += 1
         dist.all_to_all_single(recv, send)
         both = torch.cat([send, recv]).cpu().numpy()
         return both[:send.numel()], both[send.numel():]
@@ -215,6 +220,7 @@ class Comm:
     def alltoall_counts(self, counts: np.ndarray) -> np.ndarray:
         send = self._to(torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device))
         recv = torch.empty_like(send)
+        self.ncoll += 1
         dist.all_to_all_single(recv, send)
         return recv.cpu().numpy()
 
@@ -223,6 +229,7 @@ class Comm:
         self.acct(what, row * (int(sum(send_counts)) - int(send_counts[self.rank])))
         s = self._to(send)
         r = torch.empty((int(sum(recv_counts)),) + tuple(send.shape[1:]), dtype=send.dtype, device=s.device)
+        self.ncoll += 1
         dist.all_to_all_single(r, s, [int(x) for x in recv_counts], [int(x) for x in send_counts])
         return self._back(r)
 
@@ -237,10 +244,12 @@ class Comm:
         if self.cpu_coll:
             send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             r = torch.empty(int(sum(recv_sizes)), dtype=send.dtype)
+            self.ncoll += 1
             dist.all_to_all_single(r, send, [int(x) for x in recv_sizes], [int(p.numel()) for p in pieces])
             self._cp(lambda: out.copy_(r.to(out.device)))
             return out, None
         outs = list(out.split([int(x) for x in recv_sizes]))
+        self.ncoll += 1
         return out, dist.all_to_all(outs, list(pieces), async_op=True)
 
     def alltoall_into(self, pieces, outs, what='other'):
@@ -250,6 +259,7 @@ class Comm:
             send = self._cp(lambda: torch.cat([p.cpu() for p in pieces]))
             rows = [int(o.shape[0]) for o in outs]
             r = torch.empty((sum(rows),) + tuple(outs[0].shape[1:]), dtype=send.dtype)
+            self.ncoll += 1
             dist.all_to_all_single(r, send, rows, [int(p.shape[0]) for p in pieces])
 
             def back():
@@ -257,6 +267,7 @@ class Comm:
                     o.copy_(x.to(o.device))
             self._cp(back)
             return
+        self.ncoll += 1
         dist.all_to_all(list(outs), list(pieces))
 
     @staticmethod
@@ -271,9 +282,11 @@ class Comm:
         self.acct(what, 2 * (self.world - 1) * t.numel() * t.element_size() // self.world)   # ring volume
         if self.cpu_coll:
             x = self._cp(lambda: t.cpu())
+            self.ncoll += 1
             dist.all_reduce(x, op=op)
             self._cp(lambda: t.copy_(x.to(t.device)))
         else:
+            self.ncoll += 1
             dist.all_reduce(t, op=op)
 
     def allgather_array(self, arr: np.ndarray, host: bool = False) -> np.ndarray:
@@ -284,9 +297,11 @@ class Comm:
             return a.reshape(1, len(a))
         if host:
             if self.shm is not None and len(a) <= ShmMeta.SLOT:
+                self.nhost += 1
                 return self.shm.allgather(a)
             t = torch.from_numpy(a)
             out = [torch.empty_like(t) for _ in range(self.world)]
+            self.nhost += 1
             dist.all_gather(out, t, group=self.meta)
             return torch.stack(out).numpy()
         t = self._cp(lambda: torch.from_numpy(a).to(self.device))
@@ -309,10 +324,12 @@ class Comm:
 
     def broadcast_ints(self, vals, src: int) -> list[int]:
         t = self._to(self._cp(lambda: torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)))
+        self.ncoll += 1
         dist.broadcast(t, src)
         return [int(x) for x in t.cpu().tolist()]
 
     def barrier(self):
+        self.ncoll += 1
         dist.barrier()
 
 
@@ -572,6 +589,7 @@ class DistSolve:
         st = {'turn': self.turn, 'records': [], 'done': False}
         self._t = time.perf_counter()
         c.xbytes.clear()   # this step's exchanges (st['xbytes'], filled at its end)
+        c.ncoll = c.nhost = 0
         cnt = self.counts[self.turn]
         st['n_parents'] = int(cnt.sum())
         if self.done:
@@ -1043,6 +1061,7 @@ class DistSolve:
         self._turn_sync()
         self._mark(st, 'rebalance')
         st['xbytes'] = dict(c.xbytes)
+        st['collectives'] = (c.ncoll, c.nhost)   # (device-group rounds, host metadata rounds) of this step
         self.turn += 1
         st['n_kept'] = int(self.counts[-1].sum())
         return st
