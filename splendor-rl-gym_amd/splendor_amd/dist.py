@@ -388,6 +388,30 @@ class ShardNoise:
         js = np.arange(j0, j1, dtype=np.int64)
         return js[(cum[js + 1] > cum[js]) & (cum[js + 1] > a - s0)]
 
+    @staticmethod
+    def _subsegs_multi(s0, cum, rr):
+        """The union of _subsegs over the ranges rr ((k, 2): [a, e) global draw indices), sorted: one pair of
+        searchsorted calls for all of them (the step's host path waits on this between the apply and the emission)."""
+        a, e = rr[:, 0] - s0, rr[:, 1] - s0
+        keep = (e > a) & (e > 0) & (a < cum[-1])
+        if not keep.any():
+            return np.zeros(0, np.int64)
+        a, e = a[keep], e[keep]
+        j0 = np.maximum(np.searchsorted(cum, a, side='right') - 1, 0)
+        j1 = np.minimum(np.searchsorted(cum, e, side='left'), len(cum) - 1)
+        if len(a) == 1:
+            js = np.arange(j0[0], j1[0], dtype=np.int64)
+        else:   # the ranges' sub-segment intervals merged (a rank's blocks are few: a Python pass), then enumerated
+            segs = []
+            for x, y in sorted(zip(j0.tolist(), j1.tolist())):
+                if segs and x <= segs[-1][1]:
+                    segs[-1][1] = max(segs[-1][1], y)
+                elif y > x:
+                    segs.append([x, y])
+            js = (np.concatenate([np.arange(x, y, dtype=np.int64) for x, y in segs]) if segs
+                  else np.zeros(0, np.int64))
+        return js[cum[js + 1] > cum[js]]
+
     def prepare(self, A: int, N: int, all_n: np.ndarray, blocks: np.ndarray | None = None):
         """Make this rank's accepted draws [A + k_off, A + k_off + n_loc) available to its emission (k_off = the
         next_queue entries of the ranks before it).  blocks (block-cyclic slices, (world, parts) entries per block):
@@ -414,11 +438,20 @@ class ShardNoise:
                       for r in range(G)]
         send = [[] for _ in range(G)]
         recv = [[] for _ in range(G)]
-        for s0, cum, g, slot in self.chunks:
-            for r in range(G):
-                if g != me and r != me:
+        def merged(rg):   # a rank's draw ranges, adjacent ones joined (one rank's blocks are one range)
+            out = []
+            for a, e, _ in sorted(rg):
+                if e <= a:
                     continue
-                js = np.unique(np.concatenate([self._subsegs(s0, cum, a, e) for a, e, _ in ranges[r]]))
+                if out and a <= out[-1][1]:
+                    out[-1][1] = max(out[-1][1], e)
+                else:
+                    out.append([a, e])
+            return np.asarray(out, dtype=np.int64).reshape(-1, 2)
+        rarr = [merged(rg) for rg in ranges]
+        for s0, cum, g, slot in self.chunks:
+            for r in (range(G) if g == me else (me,)):
+                js = self._subsegs_multi(s0, cum, rarr[r])
                 if g == me:
                     send[r].append(slot * PS + js)
                 if r == me:
