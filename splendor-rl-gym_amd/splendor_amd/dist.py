@@ -379,19 +379,10 @@ class ShardNoise:
             self.gen_total += int(cum[-1])
 
     @staticmethod
-    def _subsegs(s0, cum, a, e):
-        """Non-empty sub-segments of a chunk holding draws with global index in [a, e)."""
-        if e <= a or s0 + cum[-1] <= a or s0 >= e:
-            return np.zeros(0, np.int64)
-        j0 = max(0, int(np.searchsorted(cum, a - s0, side='right')) - 1)
-        j1 = min(len(cum) - 1, int(np.searchsorted(cum, e - s0, side='left')))
-        js = np.arange(j0, j1, dtype=np.int64)
-        return js[(cum[js + 1] > cum[js]) & (cum[js + 1] > a - s0)]
-
-    @staticmethod
     def _subsegs_multi(s0, cum, rr):
-        """The union of _subsegs over the ranges rr ((k, 2): [a, e) global draw indices), sorted: one pair of
-        searchsorted calls for all of them (the step's host path waits on this between the apply and the emission)."""
+        """Non-empty sub-segments of a chunk (first global accepted index s0, cumulative counts cum) holding draws of
+        any of the ranges rr ((k, 2): [a, e) global indices), sorted: one pair of searchsorted calls for all of them
+        (the step's host path waits on this between the apply and the emission)."""
         a, e = rr[:, 0] - s0, rr[:, 1] - s0
         keep = (e > a) & (e > 0) & (a < cum[-1])
         if not keep.any():
