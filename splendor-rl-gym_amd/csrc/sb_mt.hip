@@ -238,9 +238,9 @@ __global__ __launch_bounds__(640) void k_mt_fill(const uint32_t* __restrict__ wi
     }
 }
 
-constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
-constexpr int JMP_NT = 1024;
-constexpr int JMP_PARTS = 8;               // poly split: 8 x 78 words
+[[maybe_unused]] constexpr int JMP_SEQ = 1 + 19937 + 624;   // y_0 .. y_{19937+623}
+[[maybe_unused]] constexpr int JMP_NT = 1024;
+[[maybe_unused]] constexpr int JMP_PARTS = 8;               // poly split: 8 x 78 words
 constexpr int JMP_JG = 10;                 // 624 outputs in groups of 64
 
 #ifndef SB_MT_JUMP_ROLL

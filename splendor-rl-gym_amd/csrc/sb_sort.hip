@@ -438,7 +438,6 @@ __global__ __launch_bounds__(1024) void k_tk_scan(uint32_t* __restrict__ gt, uin
     const int64_t ntiles = ((n_dev ? (int64_t)*n_dev : n_host) + TK_TILE - 1) / TK_TILE;
     uint32_t cg = 0, ce = 0;
     for (int64_t b = 0; b < ntiles; b += 1024 * SC_PER) {
-        const int64_t i0 = b + (int64_t)threadIdx.x * SC_PER;
         if (b > 0) __syncthreads();   // the previous chunk's LDS reads are done
 #pragma unroll
         for (int j = 0; j < SC_PER; j++) {
