@@ -821,7 +821,7 @@ class DistSolve:
                 cap = cap_j
                 b.owner_begin(cap, [0] * W)
                 with ctx():
-                    ret = b.answer_buffer(cap)
+                    ret = getattr(b, 'ret_buffer', b.answer_buffer)(cap)
                     rbuf = b.record_buffer(cap)
                 self._mark(st, 'expand')
             from_src = M[:, me]                               # records each source (this rank too) sends me
@@ -832,7 +832,8 @@ class DistSolve:
                     for hd in handles:                        # the earlier parts land before they are copied
                         c.wait(hd)
                     handles = []
-                    g_ret, g_rec = b.answer_buffer(cap), b.record_buffer(cap)
+                    g_ret, g_rec = b.answer_buffer(cap), b.record_buffer(cap)   # (new buffers: the old ones stay live
+                    # in ret / rbuf until copied)
                     if ans_base:
                         g_rec[:ans_base].copy_(rbuf[:ans_base])
                         if bc:   # the earlier parts' answers (claimed already)
@@ -1474,6 +1475,7 @@ class HipBackend:
         torch.cuda.synchronize(self.device)
 
     def close(self):
+        self._rbuf = self._abuf = self._send_t = None   # (the turn buffers kept across turns)
         if getattr(self, 'h', None):
             self.lib.sb_destroy(self.h)
             self.h = None
@@ -1624,8 +1626,21 @@ class HipBackend:
         self._chk(self.lib.sbd_owner_finish(self.h, ret.data_ptr()), 'sbd_owner_finish')
 
     def record_buffer(self, n):
-        """The turn's receive buffer of record keys (global-order claims: every part lands in it)."""
-        return self._empty(max(int(n), 1))
+        """The turn's receive buffer of record keys (global-order claims: every part lands in it): one buffer kept
+        across turns and grown only when a turn needs more, so the caching allocator is not asked for a new
+        multi-GB block whenever the bound moves (reuse is ordered like the allocator's: the previous turn's claims
+        finished on the stream before this turn's first part can arrive)."""
+        n = max(int(n), 1)
+        if getattr(self, '_rbuf', None) is None or self._rbuf.numel() < n:
+            self._rbuf = torch.empty(n + n // 8, dtype=torch.int64, device=self.device)
+        return self._rbuf[:n]
+
+    def ret_buffer(self, n):
+        """The turn's claim answers (one byte per received record), kept across turns like record_buffer."""
+        n = max(int(n), 1)
+        if getattr(self, '_abuf', None) is None or self._abuf.numel() < n:
+            self._abuf = torch.empty(n + n // 8, dtype=torch.uint8, device=self.device)
+        return self._abuf[:n]
 
     def owner_claim_all(self, rbuf, n_total, v_start, p_start, ret):
         vs = np.ascontiguousarray(v_start, dtype=np.int64)
