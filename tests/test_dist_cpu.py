@@ -49,11 +49,15 @@ def _worker(rank, world, port, cfg, outdir):
         b.goc = True
     if cfg.get('small_cap'):   # a receive bound far below the records received: the host grows it (sbd_grow_receive)
         b.recv_cap = cfg['small_cap']
+    if cfg.get('shm'):   # every rank on this node (torch.distributed.run sets it): host metadata over shared memory
+        os.environ['LOCAL_WORLD_SIZE'] = str(world)
     if cfg.get('deferred'):   # RCCL's completion contract (Comm's non-gloo branches), tests/deferred_comm.py
         from deferred_comm import DeferredComm
         comm = DeferredComm(torch.device('cpu'))
     else:
         comm = Comm(torch.device('cpu'))
+    if cfg.get('shm'):
+        assert comm.shm is not None, 'shared-memory metadata not set up'
     if cfg.get('serialize'):   # the profiling wrappers (bench_dist.py SB_DIST_SERIALIZE=1) change nothing
         from splendor_amd.dist import SerializedBackend
         b = SerializedBackend(b)
@@ -72,7 +76,8 @@ def _worker(rank, world, port, cfg, outdir):
            'slices': [[lo, hi, par] for lo, hi, par in b.turns],
            'mt': b.mt_state().tolist() if cfg['heur'] else None,
            'deferred': [comm.deferred_calls, comm.waits] if cfg.get('deferred') else None,
-           'grown': getattr(b, 'grown', 0)}
+           'grown': getattr(b, 'grown', 0), 'shm': getattr(comm, 'shm', None) is not None,
+           'collectives': [t.get('collectives') for t in trace]}
     with open(os.path.join(outdir, f'rank{rank}.json'), 'w') as f:
         json.dump(out, f)
     dist.destroy_process_group()
@@ -174,6 +179,11 @@ CASES = [
     (1, {'goal': 6, 'hid': 2, 'name': 'aggressive', 'width': 300, 'seed': 15, 'heur': True, 'parts': 4, 'goc': True}),
     (2, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 300, 'seed': 1, 'heur': True, 'parts': 3, 'goc': True,
          'gkr': False}),
+    # host metadata over shared memory (ShmMeta: the default when every rank is on one node)
+    (4, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 250, 'seed': 7, 'heur': True, 'parts': 4, 'goc': True,
+         'shm': True}),
+    (8, {'goal': 5, 'hid': 3, 'name': 'efficiency', 'width': 120, 'seed': 8, 'heur': True, 'parts': 2, 'goc': True,
+         'shm': True}),
     # part 0's blocks a third / twice the others' (SB_DIST_P0): any boundaries, the same on every rank
     (3, {'goal': 6, 'hid': 1, 'name': 'balanced', 'width': 400, 'seed': 13, 'heur': True, 'parts': 4, 'goc': True,
          'p0': 0.33}),
@@ -211,6 +221,43 @@ def test_sharded_solve_matches_oracle(world, cfg):
         assert any(r['grown'] for r in res), 'no rank grew its receive bound'
     if cfg.get('goc') and cfg['heur'] and cfg.get('parts', 0) >= 2:   # block-cyclic unless 20-byte records
         assert res[0]['bc'] == (cfg.get('gkr', True) or world == 1), res[0]['bc']
+    if cfg.get('shm'):   # the metadata went over shared memory: one host round per turn sync and per part
+        assert all(r['shm'] for r in res)
+        P = cfg['parts']
+        assert all(c is None or c[1] == 1 + P for r in res for c in r['collectives'][1:-1]), res[0]['collectives']
     if cfg.get('deferred'):   # the deferred path really ran: every rank issued async exchanges and waited for each
         assert all(r['deferred'][0] > 0 and r['deferred'][0] == r['deferred'][1] for r in res), [r['deferred'] for r in res]
     o.close()
+
+
+def _shm_worker(rank, world, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'splendor-rl-gym_amd')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from splendor_amd.dist import ShmMeta
+    dist.init_process_group('gloo', init_method='file://' + os.path.join(outdir, 'store'), rank=rank, world_size=world)
+    g = dist.new_group(backend='gloo')
+    m = ShmMeta(rank, world, g)
+    rng = np.random.default_rng(100 + rank)
+    for k in range(200):   # rounds of varying lengths (both parity slots reused many times), ranks skewed
+        n = 1 + (k * 37) % ShmMeta.SLOT
+        v = np.arange(n, dtype=np.int64) * (rank + 1) + k
+        if rng.random() < 0.1:
+            import time
+            time.sleep(0.002)
+        out = m.allgather(v)
+        exp = np.stack([np.arange(n, dtype=np.int64) * (q + 1) + k for q in range(world)])
+        assert out.shape == (world, n) and (out == exp).all(), (rank, k)
+    m.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 5])
+def test_shm_meta_allgather(world):
+    """ShmMeta (the host metadata exchange when every rank is on one node): 200 all_gathers of varying length with
+    skewed ranks return every rank's vector in rank order."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_shm_worker, args=(world, d), nprocs=world, join=True)
