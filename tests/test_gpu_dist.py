@@ -60,11 +60,15 @@ def _worker(rank, world, port, cfg, outdir):
     b = HipBackend(rank=rank, world=world, device_index=0, goal_pts=cfg['goal'], use_heuristic=cfg['heur'],
                    heuristic=cfg['hid'], beam_width=cfg['width'], mt_state625=st, visited_log2=cfg.get('vlog2', 0),
                    extra_flags=cfg.get('flags', 0))
+    if cfg.get('shm'):   # every rank on this node, as under torch.distributed.run: metadata over shared memory
+        os.environ['LOCAL_WORLD_SIZE'] = str(world)
     if cfg.get('devdeferred'):   # Comm's RCCL branches under RCCL's device-side completion contract
         from device_deferred_comm import DeviceDeferredComm
         comm = DeviceDeferredComm(b.device)
     else:
         comm = Comm(b.device)
+    if cfg.get('shm'):
+        assert comm.shm is not None
     solve = DistSolve(b, comm, goal_pts=cfg['goal'], use_heuristic=cfg['heur'], beam_width=cfg['width'])
     trace = []
     while not solve.done:
@@ -163,6 +167,7 @@ CASES = [
          'bc': True}),
     (2, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 5000, 'seed': 10, 'heur': True, 'vlog2': 10, 'bc': True}),
     (2, {'goal': 7, 'hid': 1, 'name': 'balanced', 'width': 700, 'seed': 1, 'heur': True, 'nobc': True, 'bc': False}),
+    (4, {'goal': 8, 'hid': 3, 'name': 'efficiency', 'width': 3000, 'seed': 3, 'heur': True, 'shm': True, 'bc': True}),
 ]
 
 
