@@ -965,7 +965,7 @@ struct Engine {
     uint32_t* h_pc = nullptr;             // pinned: per part, per owner record counts (16 x 64)
     uint64_t lostb_cap = 0;               // answers (received records) the lost bits / claims may index this turn
     hipStream_t s_claim = nullptr;
-    DBuf<uint32_t> ks_rdr, ks_sown, ks_cc, ks_tot, ks_pc;
+    DBuf<uint32_t> ks_rdr, ks_sown, ks_cc, ks_tot, ks_pc, ks_tk;   // ks_tk: the parts' chunk tickets
     DBuf<uint64_t> ks_send;               // global-order claims: the turn's packed records (sbd_send_buffer)
     // card-set ownership of the sharded dedup (sb_mig.inc, cfg flags bit 8): range side (parents' owner digits,
     // their rows' send positions, the partition histogram, per-owner counts), expand side (the received parents
@@ -1911,6 +1911,7 @@ void sb_destroy(sb_engine* h) {
     E.ks_cc.release();
     E.ks_tot.release();
     E.ks_pc.release();
+    E.ks_tk.release();
     E.mdig.release();
     E.mpos.release();
     E.mhist.release();
